@@ -1,0 +1,275 @@
+"""ctypes binding of libcmpc.so (the C ABI in include/cmpc.h).
+
+The shared library is built in-tree (``make -C centroidal-mpc_amd/csrc``, or
+``__graft_entry__.build()``).  There is no CPU fallback: every entry point runs on the GPU and
+a missing library or GPU raises ``CmpcError``.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libcmpc.so')
+
+ROBOTS = {'solo12': 0, 'TALOS': 1}
+PREC = {'fp64': 0, 'float64': 0, 'f64': 0, 'fp32': 1, 'float32': 1, 'f32': 1}
+QP_STATUS = {1: 'solved', -2: 'maximum iterations reached', -3: 'primal infeasible', -10: 'non-finite'}
+SCP_STATUS = {0: 'running', 1: 'converged', 2: 'max_iter', -1: 'qp_failed'}
+DECISION = {0: 'none', 1: 'accept', 2: 'reject_rho', 3: 'reject_tr', -1: 'qp_failed'}
+
+
+class CmpcError(RuntimeError):
+    pass
+
+
+class Params(ctypes.Structure):
+    _fields_ = [('mass', ctypes.c_double), ('gravity', ctypes.c_double), ('dt', ctypes.c_double),
+                ('mu', ctypes.c_double), ('beta_u', ctypes.c_double), ('foot_range', ctypes.c_double * 4),
+                ('Wx', ctypes.c_double * 9), ('Wu', ctypes.c_double * 12), ('Q', ctypes.c_double * 81),
+                ('R', ctypes.c_double * 144), ('cov_w', ctypes.c_double * 144), ('cov_eta', ctypes.c_double * 81),
+                ('stochastic', ctypes.c_int32), ('tracking', ctypes.c_int32),
+                ('tr_radius0', ctypes.c_double), ('omega0', ctypes.c_double), ('omega_max', ctypes.c_double),
+                ('rho0', ctypes.c_double), ('rho1', ctypes.c_double), ('beta_succ', ctypes.c_double),
+                ('beta_fail', ctypes.c_double), ('gamma_fail', ctypes.c_double),
+                ('convergence_threshold', ctypes.c_double), ('max_iterations', ctypes.c_int32)]
+
+
+class QPSettings(ctypes.Structure):
+    _fields_ = [('max_iter', ctypes.c_int32), ('eps_abs', ctypes.c_double), ('eps_rel', ctypes.c_double),
+                ('step_fraction', ctypes.c_double)]
+
+
+class Timing(ctypes.Structure):
+    _fields_ = [('linearize_ms', ctypes.c_float), ('assemble_ms', ctypes.c_float), ('qp_ms', ctypes.c_float),
+                ('accept_ms', ctypes.c_float), ('total_ms', ctypes.c_float)]
+
+
+EXPORTS = ['cmpc_create', 'cmpc_destroy', 'cmpc_last_error', 'cmpc_version', 'cmpc_default_qp_settings',
+           'cmpc_set_qp_settings', 'cmpc_set_params', 'cmpc_upload', 'cmpc_linearize', 'cmpc_assemble',
+           'cmpc_qp_solve', 'cmpc_accept', 'cmpc_scp_iterate', 'cmpc_solve_scp', 'cmpc_synchronize',
+           'cmpc_get_linearization', 'cmpc_qp_sizes', 'cmpc_export_qp', 'cmpc_get_qp_solution',
+           'cmpc_get_solution', 'cmpc_get_iteration_log', 'cmpc_get_timing']
+
+_lib = None
+
+
+def load():
+    """Load libcmpc.so (raises CmpcError when it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise CmpcError('libcmpc.so not found at %s: build it with `make -C centroidal-mpc_amd/csrc` '
+                        '(or __graft_entry__.build()); there is no CPU fallback' % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    P = ctypes.POINTER
+    vp = ctypes.c_void_p
+    h = ctypes.c_void_p
+    i32 = ctypes.c_int
+    sig = {
+        'cmpc_create': (i32, [P(h), i32, i32, i32, i32, i32]),
+        'cmpc_destroy': (i32, [h]),
+        'cmpc_last_error': (ctypes.c_char_p, [h]),
+        'cmpc_version': (i32, []),
+        'cmpc_default_qp_settings': (i32, [i32, P(QPSettings)]),
+        'cmpc_set_qp_settings': (i32, [h, P(QPSettings)]),
+        'cmpc_set_params': (i32, [h, i32, P(Params)]),
+        'cmpc_upload': (i32, [h, i32, vp, vp, vp, vp, vp, vp]),
+        'cmpc_linearize': (i32, [h]),
+        'cmpc_assemble': (i32, [h]),
+        'cmpc_qp_solve': (i32, [h]),
+        'cmpc_accept': (i32, [h, i32]),
+        'cmpc_scp_iterate': (i32, [h, i32]),
+        'cmpc_solve_scp': (i32, [h, i32, P(ctypes.c_int)]),
+        'cmpc_synchronize': (i32, [h]),
+        'cmpc_get_linearization': (i32, [h, vp, vp, vp, vp, vp, vp]),
+        'cmpc_qp_sizes': (i32, [h, vp, vp, vp, vp]),
+        'cmpc_export_qp': (i32, [h, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+        'cmpc_get_qp_solution': (i32, [h, vp, vp, vp, vp]),
+        'cmpc_get_solution': (i32, [h, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+        'cmpc_get_iteration_log': (i32, [h, vp, vp, vp, vp, vp]),
+        'cmpc_get_timing': (i32, [h, P(Timing)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def params_struct(p, nc):
+    """ModelParams -> Params (C struct)."""
+    s = Params()
+    s.mass, s.gravity, s.dt, s.mu, s.beta_u = p.mass, p.gravity, p.dt, p.mu, p.beta_u
+    s.foot_range[:] = list(p.foot_range)
+    s.Wx[:] = list(np.asarray(p.Wx, float))
+    s.Wu[:] = list(np.asarray(p.Wu, float))
+    s.Q[:] = list(np.asarray(p.Q, float).ravel())
+    R = np.zeros((12, 12)); R[:p.R.shape[0], :p.R.shape[1]] = p.R
+    s.R[:] = list(R.ravel())
+    W = np.zeros((12, 12)); nw = 3 * nc; W[:nw, :nw] = np.asarray(p.cov_w, float)[:nw, :nw]
+    s.cov_w[:] = list(W.ravel())
+    s.cov_eta[:] = list(np.asarray(p.cov_eta, float).ravel())
+    s.stochastic = int(bool(p.stochastic))
+    s.tracking = int(bool(p.tracking))
+    sp = p.scp_params
+    s.tr_radius0 = float(sp.get('trust_region_radius0', 100.0))
+    s.omega0 = float(sp.get('omega0', 100.0))
+    s.omega_max = float(sp.get('omega_max', 1e10))
+    s.rho0 = float(sp.get('rho0', 0.4))
+    s.rho1 = float(sp.get('rho1', 1.5))
+    s.beta_succ = float(sp.get('beta_succ', 2.0))
+    s.beta_fail = float(sp.get('beta_fail', 0.5))
+    s.gamma_fail = float(sp.get('gamma_fail', 5.0))
+    s.convergence_threshold = float(sp.get('convergence_threshold', 1e-3))
+    s.max_iterations = int(sp.get('max_iterations', 10))
+    return s
+
+
+class Solver:
+    """One device handle: B problems of one robot / horizon, resident in HBM."""
+
+    def __init__(self, robot, N, max_batch, precision='fp64', device=0):
+        self.lib = load()
+        self.robot = robot
+        self.N = int(N)
+        self.nc = 4 if robot == 'solo12' else 2
+        self.nu = 12
+        self.prec = PREC[precision]
+        self.max_batch = int(max_batch)
+        self.B = 0
+        h = ctypes.c_void_p()
+        rc = self.lib.cmpc_create(ctypes.byref(h), int(device), ROBOTS[robot], self.N, self.max_batch, self.prec)
+        if rc != 0 or not h.value:
+            raise CmpcError('cmpc_create failed (rc=%d): no usable GPU / HIP runtime?' % rc)
+        self.h = h
+
+    def _chk(self, rc, what):
+        if rc != 0:
+            msg = self.lib.cmpc_last_error(self.h)
+            raise CmpcError('%s failed (rc=%d): %s' % (what, rc, msg.decode() if msg else ''))
+
+    def close(self):
+        if getattr(self, 'h', None) is not None and self.h.value:
+            self.lib.cmpc_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- setup
+    def set_qp_settings(self, max_iter=None, eps_abs=None, eps_rel=None, step_fraction=None):
+        s = QPSettings()
+        self.lib.cmpc_default_qp_settings(self.prec, ctypes.byref(s))
+        if max_iter is not None: s.max_iter = int(max_iter)
+        if eps_abs is not None: s.eps_abs = float(eps_abs)
+        if eps_rel is not None: s.eps_rel = float(eps_rel)
+        if step_fraction is not None: s.step_fraction = float(step_fraction)
+        self._chk(self.lib.cmpc_set_qp_settings(self.h, ctypes.byref(s)), 'cmpc_set_qp_settings')
+
+    def set_params(self, params):
+        arr = (Params * len(params))(*[params_struct(p, self.nc) for p in params])
+        self._chk(self.lib.cmpc_set_params(self.h, len(params), arr), 'cmpc_set_params')
+
+    def upload(self, pb):
+        """ProblemBatch -> device (resets the SCP state of every problem)."""
+        if pb.robot != self.robot or pb.N != self.N:
+            raise CmpcError('batch robot/N (%s, %d) does not match the handle (%s, %d)'
+                            % (pb.robot, pb.N, self.robot, self.N))
+        self.set_params(pb.params)
+        self._keep = [np.ascontiguousarray(pb.class_id, np.int32), np.ascontiguousarray(pb.logic, np.int8),
+                      np.ascontiguousarray(pb.pos, float), np.ascontiguousarray(pb.rot, float),
+                      np.ascontiguousarray(pb.Xbar, float), np.ascontiguousarray(pb.Ubar, float)]
+        self._chk(self.lib.cmpc_upload(self.h, pb.B, *[_ptr(a) for a in self._keep]), 'cmpc_upload')
+        self.B = pb.B
+
+    # ---- phases
+    def linearize(self): self._chk(self.lib.cmpc_linearize(self.h), 'cmpc_linearize')
+    def assemble(self): self._chk(self.lib.cmpc_assemble(self.h), 'cmpc_assemble')
+    def qp_solve(self): self._chk(self.lib.cmpc_qp_solve(self.h), 'cmpc_qp_solve')
+    def accept(self, fixed_iters=False): self._chk(self.lib.cmpc_accept(self.h, int(fixed_iters)), 'cmpc_accept')
+
+    def scp_iterate(self, fixed_iters=True):
+        self._chk(self.lib.cmpc_scp_iterate(self.h, int(fixed_iters)), 'cmpc_scp_iterate')
+
+    def solve_scp(self, fixed_iters=False):
+        n = ctypes.c_int(0)
+        self._chk(self.lib.cmpc_solve_scp(self.h, int(fixed_iters), ctypes.byref(n)), 'cmpc_solve_scp')
+        return n.value
+
+    def synchronize(self):
+        self._chk(self.lib.cmpc_synchronize(self.h), 'cmpc_synchronize')
+
+    # ---- getters
+    def linearization(self):
+        B, N, nc = self.B, self.N, self.nc
+        out = dict(f=np.zeros((B, N, 9)), A=np.zeros((B, N, 9, 9)), Bu=np.zeros((B, N, 9, 12)),
+                   C=np.zeros((B, N, 9, 3 * nc)), K=np.zeros((B, N, 12, 9)), Sigma=np.zeros((B, N + 1, 9, 9)))
+        self._chk(self.lib.cmpc_get_linearization(self.h, *[_ptr(out[k]) for k in ('f', 'A', 'Bu', 'C', 'K', 'Sigma')]),
+                  'cmpc_get_linearization')
+        return out
+
+    def qp_sizes(self):
+        v = [np.zeros(1, np.int32) for _ in range(4)]
+        self._chk(self.lib.cmpc_qp_sizes(self.h, *[_ptr(a) for a in v]), 'cmpc_qp_sizes')
+        return tuple(int(a[0]) for a in v)
+
+    def export_qp(self, b):
+        """(P, q, A, l, u) of problem b as scipy CSC, in the reference's row order."""
+        from scipy import sparse
+        n, m, nnzP, nnzA = self.qp_sizes()
+        Px = np.zeros(nnzP); Pi = np.zeros(nnzP, np.int32); Pp = np.zeros(n + 1, np.int32)
+        q = np.zeros(n)
+        Ax = np.zeros(nnzA); Ai = np.zeros(nnzA, np.int32); Ap = np.zeros(n + 1, np.int32)
+        l = np.zeros(m); u = np.zeros(m)
+        self._chk(self.lib.cmpc_export_qp(self.h, int(b), *[_ptr(a) for a in (Px, Pi, Pp, q, Ax, Ai, Ap, l, u)]),
+                  'cmpc_export_qp')
+        P = sparse.csc_matrix((Px[:Pp[-1]], Pi[:Pp[-1]], Pp), shape=(n, n))
+        A = sparse.csc_matrix((Ax[:Ap[-1]], Ai[:Ap[-1]], Ap), shape=(m, n))
+        return P, q, A, l, u
+
+    def qp_solution(self, with_y=True):
+        n, m, _, _ = self.qp_sizes()
+        z = np.zeros((self.B, n)); y = np.zeros((self.B, m)) if with_y else None
+        st = np.zeros(self.B, np.int32); it = np.zeros(self.B, np.int32)
+        self._chk(self.lib.cmpc_get_qp_solution(self.h, _ptr(z), _ptr(y), _ptr(st), _ptr(it)), 'cmpc_get_qp_solution')
+        return z, y, st, it
+
+    def solution(self):
+        B, N = self.B, self.N
+        out = dict(X=np.zeros((B, N + 1, 9)), U=np.zeros((B, N, 12)), K=np.zeros((B, N, 12, 9)),
+                   Sigma=np.zeros((B, N + 1, 9, 9)), n_accepted=np.zeros(B, np.int32),
+                   iterations=np.zeros(B, np.int32), status=np.zeros(B, np.int32), weight=np.zeros(B),
+                   radius=np.zeros(B))
+        keys = ('X', 'U', 'K', 'Sigma', 'n_accepted', 'iterations', 'status', 'weight', 'radius')
+        self._chk(self.lib.cmpc_get_solution(self.h, *[_ptr(out[k]) for k in keys]), 'cmpc_get_solution')
+        return out
+
+    def iteration_log(self):
+        B = self.B
+        out = dict(tr_norm=np.zeros(B), rho=np.zeros(B), qp_status=np.zeros(B, np.int32),
+                   qp_iters=np.zeros(B, np.int32), decision=np.zeros(B, np.int32))
+        keys = ('tr_norm', 'rho', 'qp_status', 'qp_iters', 'decision')
+        self._chk(self.lib.cmpc_get_iteration_log(self.h, *[_ptr(out[k]) for k in keys]), 'cmpc_get_iteration_log')
+        return out
+
+    def timing(self):
+        t = Timing()
+        self._chk(self.lib.cmpc_get_timing(self.h, ctypes.byref(t)), 'cmpc_get_timing')
+        return dict(linearize_ms=t.linearize_ms, assemble_ms=t.assemble_ms, qp_ms=t.qp_ms,
+                    accept_ms=t.accept_ms, total_ms=t.total_ms)

@@ -1,0 +1,59 @@
+"""Solo12 trot (reference config/conf_solo12_trot.py, same attribute names and values)."""
+import numpy as np
+
+from src.contact_plan import create_contact_sequence, plan_length
+from config import _robots
+
+# walking parameters (:7-19)
+DYNAMICS_FIRST = False
+dt = 0.01
+dt_ctrl = 0.001
+gait = {'type': 'TROT', 'stepLength': 0.12, 'stepHeight': 0.1, 'stepKnots': 15, 'supportKnots': 5,
+        'nbSteps': 4}
+mu = 0.5
+
+# robot model and parameters (:21-36)
+robot_name = 'solo12'
+ee_frame_names = ['FL_FOOT', 'FR_FOOT', 'HL_FOOT', 'HR_FOOT']
+rmodel, rdata, q0, robot_mass = _robots.solo12()
+gravity_constant = -9.81
+max_leg_length = 0.34
+foot_scaling = 1.
+lxp = lxn = lyp = lyn = 0.01
+
+# centroidal state and control dimensions (:38-43)
+n_u_per_contact = 3
+nb_contacts = 4
+n_u = nb_contacts * n_u_per_contact
+n_x = 9
+n_t = 1
+
+gait_templates, contact_sequence = create_contact_sequence(dt, gait, ee_frame_names, rmodel, rdata, q0)
+N = plan_length(contact_sequence, dt)
+N_ctrl = int((N - 1) * (dt / dt_ctrl))
+
+# LQR gains (:55-62)
+Q = np.diag([1e4, 1e4, 1e4, 1e3, 1e3, 1e3, 1e3, 1e3, 1e3])
+R = np.diag([1e2, 1e3, 1e1] * 4)
+
+# noise (:66-77)
+n_w = nb_contacts * 3
+cov_w = np.diag([0.4 ** 2, 0.4 ** 2, 0.1 ** 2] * 4)
+cov_white_noise = dt * np.diag(np.array([0.85 ** 2, 0.4 ** 2, 0.01 ** 2, 0.75 ** 2, 0.4 ** 2, 0.01 ** 2,
+                                         0.85 ** 2, 0.4 ** 2, 0.01 ** 2]))
+beta_u = 0.01
+
+# cost weights (:81-85)
+state_cost_weights = np.diag([1e4, 1e4, 1e4, 1e3, 1e3, 1e3, 1e5, 1e5, 1e5])
+control_cost_weights = np.diag([1e0, 1e2, 1e1] * 4)
+
+# SCP solver parameters (:93-94)
+scp_params = {'trust_region_radius0': 100, 'omega0': 100, 'omega_max': 1e10, 'epsilon': 1e-6, 'rho0': 0.4,
+              'rho1': 1.5, 'beta_succ': 2., 'beta_fail': 0.5, 'gamma_fail': 5, 'convergence_threshold': 1e-3,
+              'max_iterations': 10}
+
+WITHDISPLAY = False
+WITH_MESHCAT_DISPLAY = False
+WITH_PYBULLET_SIMULATION = False
+WITHPLOT = False
+SAVEDAT = False

@@ -1,0 +1,666 @@
+// C ABI of libcmpc.so (declared in include/cmpc.h): handle lifecycle, device memory, kernel
+// launches and the host-side CSC export used for parity tests.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "cmpc.h"
+#include "common.hpp"
+
+namespace cmpc {
+template <typename T, int R> __global__ void k_linearize(DevBuf<T>, int);
+template <typename T, int R> __global__ void k_assemble(DevBuf<T>, int);
+template <typename T, int R> __global__ void k_qp_ipm(DevBuf<T>, int, int, T, T, T);
+template <typename T, int R> __global__ void k_accept(DevBuf<T>, int);
+size_t ipm_workspace_elems(int N, int robot);
+}  // namespace cmpc
+
+using namespace cmpc;
+
+namespace {
+
+struct Fail {
+    int code;
+    std::string msg;
+};
+
+#define HIPCHK(x)                                                                                   \
+    do {                                                                                            \
+        hipError_t e_ = (x);                                                                        \
+        if (e_ != hipSuccess) throw Fail{-3, std::string(#x) + ": " + hipGetErrorString(e_)};      \
+    } while (0)
+
+// Inverse standard normal CDF (Acklam's rational approximation refined by Halley steps on
+// erfc), to reproduce scipy.stats.norm.ppf for xi (reference src/constraints.py:157).
+double norm_ppf(double p) {
+    static const double a[] = {-3.969683028665376e+01, 2.209460984245205e+02, -2.759285104469687e+02,
+                               1.383577518672690e+02, -3.066479806614716e+01, 2.506628277459239e+00};
+    static const double b[] = {-5.447609879822406e+01, 1.615858368580409e+02, -1.556989798598866e+02,
+                               6.680131188771972e+01, -1.328068155288572e+01};
+    static const double c[] = {-7.784894002430293e-03, -3.223964580411365e-01, -2.400758277161838e+00,
+                               -2.549732539343734e+00, 4.374664141464968e+00, 2.938163982698783e+00};
+    static const double d[] = {7.784695709041462e-03, 3.224671290700398e-01, 2.445134137142996e+00,
+                               3.754408661907416e+00};
+    double x;
+    const double pl = 0.02425;
+    if (p < pl) {
+        double q = std::sqrt(-2 * std::log(p));
+        x = (((((c[0] * q + c[1]) * q + c[2]) * q + c[3]) * q + c[4]) * q + c[5]) /
+            ((((d[0] * q + d[1]) * q + d[2]) * q + d[3]) * q + 1);
+    } else if (p <= 1 - pl) {
+        double q = p - 0.5, r = q * q;
+        x = (((((a[0] * r + a[1]) * r + a[2]) * r + a[3]) * r + a[4]) * r + a[5]) * q /
+            (((((b[0] * r + b[1]) * r + b[2]) * r + b[3]) * r + b[4]) * r + 1);
+    } else {
+        double q = std::sqrt(-2 * std::log(1 - p));
+        x = -(((((c[0] * q + c[1]) * q + c[2]) * q + c[3]) * q + c[4]) * q + c[5]) /
+            ((((d[0] * q + d[1]) * q + d[2]) * q + d[3]) * q + 1);
+    }
+    for (int i = 0; i < 3; ++i) {
+        double e = 0.5 * std::erfc(-x / std::sqrt(2.0)) - p;
+        double u = e * std::sqrt(2 * M_PI) * std::exp(x * x / 2);
+        x = x - u / (1 + x * u / 2);
+    }
+    return x;
+}
+
+}  // namespace
+
+struct cmpc_handle_s {
+    int device = 0, robot = 0, N = 0, max_batch = 0, prec = 0, B = 0, n_classes = 0;
+    int NC = 4, NI = 25, SS = 160;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[5] = {};
+    bool timed = false;
+    std::string err;
+    cmpc_qp_settings qs{};
+    std::vector<cmpc_params> hparams;
+    std::vector<void *> allocs;
+    size_t ws_stride = 0;
+    // device pointers (typed by precision at use)
+    void *class_id = nullptr, *params = nullptr, *logic = nullptr, *pos = nullptr, *rot = nullptr, *Xbar = nullptr,
+         *Ubar = nullptr, *f = nullptr, *A = nullptr, *Bu = nullptr, *C = nullptr, *K = nullptr, *Sig = nullptr,
+         *Acl = nullptr, *Qw = nullptr, *stage = nullptr, *cw = nullptr, *xs = nullptr, *us = nullptr, *ts = nullptr,
+         *nus = nullptr, *lams = nullptr, *qp_status = nullptr, *qp_iters = nullptr, *ws = nullptr, *scp = nullptr,
+         *Xacc = nullptr, *Uacc = nullptr, *Kacc = nullptr, *Sacc = nullptr;
+
+    size_t esz() const { return prec == CMPC_PREC_F64 ? 8 : 4; }
+    void *dalloc(size_t bytes) {
+        void *p = nullptr;
+        HIPCHK(hipMalloc(&p, std::max<size_t>(bytes, 16)));
+        HIPCHK(hipMemsetAsync(p, 0, std::max<size_t>(bytes, 16), stream));
+        allocs.push_back(p);
+        return p;
+    }
+    template <typename T> DevBuf<T> buf() const {
+        DevBuf<T> d;
+        d.B = B; d.N = N;
+        d.class_id = (const int32_t *)class_id; d.params = (const DevParams<T> *)params;
+        d.logic = (const uint8_t *)logic; d.pos = (const T *)pos; d.rot = (const T *)rot;
+        d.Xbar = (const T *)Xbar; d.Ubar = (const T *)Ubar;
+        d.f = (T *)f; d.A = (T *)A; d.Bu = (T *)Bu; d.C = (T *)C; d.K = (T *)K; d.Sig = (T *)Sig;
+        d.Acl = (T *)Acl; d.Qw = (T *)Qw; d.stage = (T *)stage; d.cw = (T *)cw;
+        d.xs = (T *)xs; d.us = (T *)us; d.ts = (T *)ts; d.nus = (T *)nus; d.lams = (T *)lams;
+        d.qp_status = (int32_t *)qp_status; d.qp_iters = (int32_t *)qp_iters;
+        d.ws = (T *)ws; d.ws_stride = ws_stride; d.scp = (ScpState *)scp;
+        d.Xacc = (T *)Xacc; d.Uacc = (T *)Uacc; d.Kacc = (T *)Kacc; d.Sacc = (T *)Sacc;
+        return d;
+    }
+};
+
+namespace {
+
+template <typename F> int guard(cmpc_handle h, F &&fn) {
+    try {
+        if (!h) return -1;
+        HIPCHK(hipSetDevice(h->device));
+        fn();
+        h->err.clear();
+        return 0;
+    } catch (const Fail &f) {
+        if (h) h->err = f.msg;
+        return f.code;
+    } catch (const std::exception &e) {
+        if (h) h->err = e.what();
+        return -9;
+    }
+}
+
+void need(bool ok, const std::string &msg) {
+    if (!ok) throw Fail{-2, msg};
+}
+
+template <typename T> void to_dev(cmpc_handle h, void *dst, const double *src, size_t n) {
+    if (sizeof(T) == 8) {
+        HIPCHK(hipMemcpyAsync(dst, src, n * 8, hipMemcpyHostToDevice, h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+    } else {
+        std::vector<T> tmp(n);
+        for (size_t i = 0; i < n; ++i) tmp[i] = T(src[i]);
+        HIPCHK(hipMemcpyAsync(dst, tmp.data(), n * sizeof(T), hipMemcpyHostToDevice, h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+    }
+}
+
+template <typename T> void from_dev(cmpc_handle h, double *dst, const void *src, size_t n) {
+    if (!dst) return;
+    if (sizeof(T) == 8) {
+        HIPCHK(hipMemcpyAsync(dst, src, n * 8, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+    } else {
+        std::vector<T> tmp(n);
+        HIPCHK(hipMemcpyAsync(tmp.data(), src, n * sizeof(T), hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+        for (size_t i = 0; i < n; ++i) dst[i] = double(tmp[i]);
+    }
+}
+
+void from_dev_raw(cmpc_handle h, void *dst, const void *src, size_t bytes) {
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+}
+
+template <typename T> DevParams<T> conv_params(const cmpc_params &p, int nw) {
+    DevParams<T> d{};
+    d.mass = T(p.mass); d.gravity = T(p.gravity); d.dt = T(p.dt); d.mu = T(p.mu);
+    d.xi = T(norm_ppf(1.0 - (p.beta_u / 5.0 * 3.0)));
+    for (int i = 0; i < 4; ++i) d.foot_range[i] = T(p.foot_range[i]);
+    for (int i = 0; i < 9; ++i) d.Wx[i] = T(p.Wx[i]);
+    for (int i = 0; i < 12; ++i) d.Wu[i] = T(p.Wu[i]);
+    for (int i = 0; i < 81; ++i) { d.Q[i] = T(p.Q[i]); d.cov_eta[i] = T(p.cov_eta[i]); }
+    for (int i = 0; i < 144; ++i) d.R[i] = T(p.R[i]);
+    // cov_w arrives as a 12x12 row-major buffer whose top-left nw x nw corner is used
+    for (int i = 0; i < nw; ++i)
+        for (int j = 0; j < nw; ++j) d.cov_w[i * nw + j] = T(p.cov_w[i * 12 + j]);
+    d.stochastic = p.stochastic; d.tracking = p.tracking;
+    d.tr_radius0 = p.tr_radius0; d.omega0 = p.omega0; d.omega_max = p.omega_max; d.rho0 = p.rho0;
+    d.rho1 = p.rho1; d.beta_succ = p.beta_succ; d.beta_fail = p.beta_fail; d.gamma_fail = p.gamma_fail;
+    d.conv_thr = p.convergence_threshold; d.max_iterations = p.max_iterations;
+    return d;
+}
+
+template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int only_active) {
+    DevBuf<T> d = h->buf<T>();
+    const int B = h->B;
+    if (B == 0) return;
+    switch (phase) {
+    case 0:
+        hipLaunchKernelGGL((k_linearize<T, R>), dim3(B), dim3(256), 0, h->stream, d, only_active);
+        break;
+    case 1: {
+        const long n = (long)B * (h->N + 1);
+        hipLaunchKernelGGL((k_assemble<T, R>), dim3((unsigned)((n + 127) / 128)), dim3(128), 0, h->stream, d,
+                           only_active);
+        break;
+    }
+    case 2:
+        hipLaunchKernelGGL((k_qp_ipm<T, R>), dim3(B), dim3(256), 0, h->stream, d, only_active, h->qs.max_iter,
+                           T(h->qs.eps_abs), T(h->qs.eps_rel), T(h->qs.step_fraction));
+        break;
+    case 3:
+        hipLaunchKernelGGL((k_accept<T, R>), dim3(B), dim3(256), 0, h->stream, d, only_active ? 0 : 1);
+        break;
+    }
+    HIPCHK(hipGetLastError());
+}
+
+void phase(cmpc_handle h, int ph, int only_active) {
+    need(h->B > 0, "no problems uploaded");
+    need(h->n_classes > 0, "parameters not set");
+    if (h->prec == CMPC_PREC_F64) {
+        if (h->robot == 0) launch_phase<double, 0>(h, ph, only_active); else launch_phase<double, 1>(h, ph, only_active);
+    } else {
+        if (h->robot == 0) launch_phase<float, 0>(h, ph, only_active); else launch_phase<float, 1>(h, ph, only_active);
+    }
+}
+
+void reset_scp(cmpc_handle h, const int32_t *class_id) {
+    std::vector<ScpState> st(h->B);
+    for (int b = 0; b < h->B; ++b) {
+        const cmpc_params &p = h->hparams[class_id[b]];
+        ScpState s{};
+        s.weight = p.omega0; s.radius = p.tr_radius0; s.active = 1; s.status = CMPC_SCP_RUNNING;
+        st[b] = s;
+    }
+    HIPCHK(hipMemcpyAsync(h->scp, st.data(), st.size() * sizeof(ScpState), hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+}
+
+std::vector<ScpState> get_scp(cmpc_handle h) {
+    std::vector<ScpState> st(h->B);
+    from_dev_raw(h, st.data(), h->scp, st.size() * sizeof(ScpState));
+    return st;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cmpc_version(void) { return 1; }
+
+const char *cmpc_last_error(cmpc_handle h) { return h ? h->err.c_str() : "null handle"; }
+
+int cmpc_default_qp_settings(int precision, cmpc_qp_settings *s) {
+    if (!s) return -1;
+    s->max_iter = precision == CMPC_PREC_F64 ? 60 : 40;
+    s->eps_abs = precision == CMPC_PREC_F64 ? 1e-9 : 1e-5;
+    s->eps_rel = precision == CMPC_PREC_F64 ? 1e-9 : 1e-5;
+    s->step_fraction = 0.99;
+    return 0;
+}
+
+int cmpc_create(cmpc_handle *out, int device, int robot, int N, int max_batch, int precision) {
+    if (!out) return -1;
+    *out = nullptr;
+    if (robot != 0 && robot != 1) return -2;
+    if (N < 2 || N > 255 || max_batch < 1) return -2;
+    if (precision != CMPC_PREC_F64 && precision != CMPC_PREC_F32) return -2;
+    cmpc_handle h = new cmpc_handle_s();
+    h->device = device; h->robot = robot; h->N = N; h->max_batch = max_batch; h->prec = precision;
+    h->NC = robot == 0 ? 4 : 2;
+    h->NI = 25;
+    h->SS = robot == 0 ? Stage<0>::SIZE : Stage<1>::SIZE;
+    cmpc_default_qp_settings(precision, &h->qs);
+    int rc = guard(h, [&] {
+        int ndev = 0;
+        HIPCHK(hipGetDeviceCount(&ndev));
+        need(device >= 0 && device < ndev, "invalid device id");
+        HIPCHK(hipSetDevice(device));
+        HIPCHK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+        for (auto &e : h->ev) HIPCHK(hipEventCreate(&e));
+        const size_t Bm = max_batch, K1 = N + 1, NB = N + 2, e = h->esz(), NC = h->NC;
+        h->class_id = h->dalloc(Bm * 4);
+        h->logic = h->dalloc(Bm * N * NC);
+        h->pos = h->dalloc(Bm * N * NC * 3 * e);
+        h->rot = h->dalloc(Bm * N * NC * 9 * e);
+        h->Xbar = h->dalloc(Bm * K1 * 9 * e);
+        h->Ubar = h->dalloc(Bm * N * NU * e);
+        h->f = h->dalloc(Bm * N * 9 * e);
+        h->A = h->dalloc(Bm * N * 81 * e);
+        h->Bu = h->dalloc(Bm * N * 9 * NU * e);
+        h->C = h->dalloc(Bm * N * 9 * 3 * NC * e);
+        h->K = h->dalloc(Bm * N * NU * 9 * e);
+        h->Sig = h->dalloc(Bm * K1 * 81 * e);
+        h->Acl = h->dalloc(Bm * N * 81 * e);
+        h->Qw = h->dalloc(Bm * N * 81 * e);
+        h->stage = h->dalloc(Bm * K1 * h->SS * e);
+        h->cw = h->dalloc(Bm * e);
+        h->xs = h->dalloc(Bm * K1 * 9 * e);
+        h->us = h->dalloc(Bm * N * NU * e);
+        h->ts = h->dalloc(Bm * K1 * e);
+        h->nus = h->dalloc(Bm * NB * 9 * e);
+        h->lams = h->dalloc(Bm * K1 * h->NI * e);
+        h->qp_status = h->dalloc(Bm * 4);
+        h->qp_iters = h->dalloc(Bm * 4);
+        h->ws_stride = ipm_workspace_elems(N, robot);
+        h->ws = h->dalloc(Bm * h->ws_stride * e);
+        h->scp = h->dalloc(Bm * sizeof(ScpState));
+        h->Xacc = h->dalloc(Bm * K1 * 9 * e);
+        h->Uacc = h->dalloc(Bm * N * NU * e);
+        h->Kacc = h->dalloc(Bm * N * NU * 9 * e);
+        h->Sacc = h->dalloc(Bm * K1 * 81 * e);
+        HIPCHK(hipStreamSynchronize(h->stream));
+    });
+    if (rc != 0) {
+        std::fprintf(stderr, "cmpc_create: %s\n", h->err.c_str());
+        cmpc_destroy(h);
+        return rc;
+    }
+    *out = h;
+    return 0;
+}
+
+int cmpc_destroy(cmpc_handle h) {
+    if (!h) return 0;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    for (void *p : h->allocs) (void)hipFree(p);
+    for (auto &e : h->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+    return 0;
+}
+
+int cmpc_set_qp_settings(cmpc_handle h, const cmpc_qp_settings *s) {
+    return guard(h, [&] {
+        need(s && s->max_iter > 0 && s->step_fraction > 0 && s->step_fraction < 1, "invalid QP settings");
+        h->qs = *s;
+    });
+}
+
+int cmpc_set_params(cmpc_handle h, int n_classes, const cmpc_params *classes) {
+    return guard(h, [&] {
+        need(n_classes > 0 && classes, "no parameter classes");
+        for (int i = 0; i < n_classes; ++i) {
+            const cmpc_params &p = classes[i];
+            need(p.mass > 0 && p.dt > 0 && p.mu > 0, "invalid mass/dt/mu");
+            for (int j = 0; j < 9; ++j) need(p.Wx[j] > 0, "state_cost_weights must be positive");
+            for (int j = 0; j < 12; ++j) need(p.Wu[j] > 0, "control_cost_weights must be positive");
+            need(p.omega0 > 0 && p.tr_radius0 > 0 && p.max_iterations > 0, "invalid scp_params");
+        }
+        h->hparams.assign(classes, classes + n_classes);
+        h->n_classes = n_classes;
+        const int nw = 3 * h->NC;
+        if (h->params) { HIPCHK(hipFree(h->params)); h->allocs.erase(std::find(h->allocs.begin(), h->allocs.end(), h->params)); }
+        if (h->prec == CMPC_PREC_F64) {
+            std::vector<DevParams<double>> v;
+            for (int i = 0; i < n_classes; ++i) v.push_back(conv_params<double>(classes[i], nw));
+            h->params = h->dalloc(v.size() * sizeof(v[0]));
+            HIPCHK(hipMemcpyAsync(h->params, v.data(), v.size() * sizeof(v[0]), hipMemcpyHostToDevice, h->stream));
+        } else {
+            std::vector<DevParams<float>> v;
+            for (int i = 0; i < n_classes; ++i) v.push_back(conv_params<float>(classes[i], nw));
+            h->params = h->dalloc(v.size() * sizeof(v[0]));
+            HIPCHK(hipMemcpyAsync(h->params, v.data(), v.size() * sizeof(v[0]), hipMemcpyHostToDevice, h->stream));
+        }
+        HIPCHK(hipStreamSynchronize(h->stream));
+    });
+}
+
+int cmpc_upload(cmpc_handle h, int B, const int32_t *class_id, const int8_t *logic, const double *pos,
+                const double *rot, const double *Xbar, const double *Ubar) {
+    return guard(h, [&] {
+        need(h->n_classes > 0, "call cmpc_set_params first");
+        need(B >= 1 && B <= h->max_batch, "batch size out of range");
+        need(class_id && logic && pos && rot && Xbar && Ubar, "null input buffer");
+        const int N = h->N, NC = h->NC;
+        for (int b = 0; b < B; ++b) need(class_id[b] >= 0 && class_id[b] < h->n_classes, "class_id out of range");
+        for (size_t k = 0; k < (size_t)B * N; ++k) {
+            int act = 0;
+            for (int c = 0; c < NC; ++c) {
+                need(logic[k * NC + c] == 0 || logic[k * NC + c] == 1, "contact logic must be 0/1");
+                act += logic[k * NC + c];
+            }
+            need(act > 0, "a knot without active contact (the reference divides by zero there)");
+        }
+        h->B = B;
+        HIPCHK(hipMemcpyAsync(h->class_id, class_id, (size_t)B * 4, hipMemcpyHostToDevice, h->stream));
+        HIPCHK(hipMemcpyAsync(h->logic, logic, (size_t)B * N * NC, hipMemcpyHostToDevice, h->stream));
+        auto up = [&](void *dst, const double *src, size_t n) {
+            if (h->prec == CMPC_PREC_F64) to_dev<double>(h, dst, src, n); else to_dev<float>(h, dst, src, n);
+        };
+        up(h->pos, pos, (size_t)B * N * NC * 3);
+        up(h->rot, rot, (size_t)B * N * NC * 9);
+        up(h->Xbar, Xbar, (size_t)B * (N + 1) * 9);
+        up(h->Ubar, Ubar, (size_t)B * N * NU);
+        reset_scp(h, class_id);
+    });
+}
+
+int cmpc_linearize(cmpc_handle h) { return guard(h, [&] { phase(h, 0, 0); }); }
+int cmpc_assemble(cmpc_handle h) { return guard(h, [&] { phase(h, 1, 0); }); }
+int cmpc_qp_solve(cmpc_handle h) { return guard(h, [&] { phase(h, 2, 0); }); }
+int cmpc_accept(cmpc_handle h, int fixed_iters) { return guard(h, [&] { phase(h, 3, fixed_iters ? 0 : 1); }); }
+
+int cmpc_scp_iterate(cmpc_handle h, int fixed_iters) {
+    return guard(h, [&] {
+        const int oa = fixed_iters ? 0 : 1;
+        HIPCHK(hipEventRecord(h->ev[0], h->stream));
+        phase(h, 0, oa);
+        HIPCHK(hipEventRecord(h->ev[1], h->stream));
+        phase(h, 1, oa);
+        HIPCHK(hipEventRecord(h->ev[2], h->stream));
+        phase(h, 2, oa);
+        HIPCHK(hipEventRecord(h->ev[3], h->stream));
+        phase(h, 3, oa);
+        HIPCHK(hipEventRecord(h->ev[4], h->stream));
+        h->timed = true;
+    });
+}
+
+int cmpc_solve_scp(cmpc_handle h, int fixed_iters, int *n_iterations_out) {
+    return guard(h, [&] {
+        int maxit = 0;
+        for (auto &p : h->hparams) maxit = std::max(maxit, p.max_iterations);
+        int it = 0;
+        for (; it < maxit; ++it) {
+            if (cmpc_scp_iterate(h, fixed_iters) != 0) throw Fail{-3, h->err};
+            if (!fixed_iters) {
+                auto st = get_scp(h);
+                bool any = false;
+                for (auto &s : st) any |= s.active != 0;
+                if (!any) { ++it; break; }
+            }
+        }
+        HIPCHK(hipStreamSynchronize(h->stream));
+        if (n_iterations_out) *n_iterations_out = it;
+    });
+}
+
+int cmpc_synchronize(cmpc_handle h) { return guard(h, [&] { HIPCHK(hipStreamSynchronize(h->stream)); }); }
+
+int cmpc_get_linearization(cmpc_handle h, double *f, double *A, double *Bu, double *C, double *K, double *Sigma) {
+    return guard(h, [&] {
+        const size_t B = h->B, N = h->N, NC = h->NC;
+        auto dl = [&](double *dst, void *src, size_t n) {
+            if (h->prec == CMPC_PREC_F64) from_dev<double>(h, dst, src, n); else from_dev<float>(h, dst, src, n);
+        };
+        dl(f, h->f, B * N * 9);
+        dl(A, h->A, B * N * 81);
+        dl(Bu, h->Bu, B * N * 9 * NU);
+        dl(C, h->C, B * N * 9 * 3 * NC);
+        dl(K, h->K, B * N * NU * 9);
+        dl(Sigma, h->Sig, B * (N + 1) * 81);
+    });
+}
+
+int cmpc_qp_sizes(cmpc_handle h, int32_t *n, int32_t *m, int32_t *nnzP, int32_t *nnzA) {
+    return guard(h, [&] {
+        const int N = h->N, NC = h->NC;
+        if (n) *n = 9 * (N + 1) + NU * N + (N + 1) + N;
+        const int mcop = h->robot == 1 ? 2 * NC * N : 0;
+        if (m) *m = 9 + 9 * N + 9 + mcop + 5 * NC * N + 8 * (N + 1) + (N + 1);
+        if (nnzP) *nnzP = 9 * (N + 1) + NU * N;
+        // upper bound on stored entries (explicit zeros are dropped at export)
+        if (nnzA) *nnzA = 9 + 9 * N * (9 + NU + 1) + 9 + mcop + 4 * 3 * NC * N + 4 * 8 * (N + 1) + (N + 1);
+    });
+}
+
+int cmpc_export_qp(cmpc_handle h, int b, double *P_x, int32_t *P_i, int32_t *P_p, double *q, double *A_x,
+                   int32_t *A_i, int32_t *A_p, double *l, double *u) {
+    return guard(h, [&] {
+        need(b >= 0 && b < h->B, "problem index out of range");
+        const int N = h->N, NC = h->NC, K1 = N + 1, NUPC = NU / NC, FO = h->robot == 0 ? 0 : 2, SS = h->SS;
+        const int n = 9 * K1 + NU * N + K1 + N;
+        auto dl = [&](std::vector<double> &dst, void *src, size_t off, size_t cnt) {
+            dst.resize(cnt);
+            const size_t e = h->esz();
+            if (h->prec == CMPC_PREC_F64) from_dev<double>(h, dst.data(), (char *)src + off * e, cnt);
+            else from_dev<float>(h, dst.data(), (char *)src + off * e, cnt);
+        };
+        std::vector<double> st, A, Bm, xb;
+        dl(st, h->stage, (size_t)b * K1 * SS, (size_t)K1 * SS);
+        dl(A, h->A, (size_t)b * N * 81, (size_t)N * 81);
+        dl(Bm, h->Bu, (size_t)b * N * 9 * NU, (size_t)N * 9 * NU);
+        dl(xb, h->Xbar, (size_t)b * K1 * 9, (size_t)K1 * 9);
+        std::vector<int8_t> lg((size_t)N * NC);
+        from_dev_raw(h, lg.data(), (char *)h->logic + (size_t)b * N * NC, lg.size());
+        int32_t cid = 0;
+        from_dev_raw(h, &cid, (char *)h->class_id + (size_t)b * 4, 4);
+        const cmpc_params &p = h->hparams[cid];
+        ScpState sc;
+        from_dev_raw(h, &sc, (char *)h->scp + (size_t)b * sizeof(ScpState), sizeof(ScpState));
+        const double cw = -1.0 / sc.weight;
+        auto xi = [&](int k) { return 9 * k; };
+        auto ui = [&](int k) { return 9 * K1 + NU * k; };
+        auto ti = [&](int k) { return 9 * K1 + NU * N + k; };
+        // ---- P (diagonal) and q
+        int pp = 0;
+        for (int c = 0; c < n; ++c) {
+            P_p[c] = pp;
+            double v = 0;
+            if (c < 9 * K1) v = p.Wx[c % 9];
+            else if (c < 9 * K1 + NU * N) v = p.Wu[(c - 9 * K1) % NU];
+            if (v != 0) { P_x[pp] = v; P_i[pp] = c; ++pp; }
+        }
+        P_p[n] = pp;
+        for (int c = 0; c < n; ++c) q[c] = 0;
+        for (int k = 0; k < K1; ++k)
+            for (int i = 0; i < 9; ++i) q[xi(k) + i] = st[(size_t)k * SS + 9 + i];
+        for (int k = 0; k < K1; ++k) q[ti(k)] = 1.0;
+        // ---- A rows in the reference order
+        std::vector<std::tuple<int, int, double>> tr;   // (col, row, val)
+        int row = 0;
+        const double inf = INFINITY;
+        auto add = [&](int c, double v) { if (v != 0.0) tr.emplace_back(c, row, v); };
+        for (int i = 0; i < 9; ++i, ++row) { add(xi(0) + i, 1.0); l[row] = u[row] = xb[i]; }
+        for (int k = 0; k < N; ++k)
+            for (int i = 0; i < 9; ++i, ++row) {
+                for (int j = 0; j < 9; ++j) add(xi(k) + j, A[(size_t)k * 81 + i * 9 + j]);
+                for (int j = 0; j < NU; ++j) add(ui(k) + j, Bm[(size_t)k * 9 * NU + i * NU + j]);
+                add(xi(k + 1) + i, -1.0);
+                const double r = st[(size_t)k * SS + i];
+                l[row] = r - 1e-12; u[row] = r + 1e-12;
+            }
+        for (int i = 0; i < 9; ++i, ++row) { add(xi(N) + i, 1.0); l[row] = u[row] = xb[(size_t)N * 9 + i]; }
+        if (h->robot == 1) {
+            for (int c = 0; c < NC; ++c)
+                for (int dd = 0; dd < 2; ++dd)
+                    for (int k = 0; k < N; ++k, ++row) {
+                        if (lg[(size_t)k * NC + c]) {
+                            add(ui(k) + NUPC * c + dd, 1.0);
+                            l[row] = -p.foot_range[dd == 0 ? 1 : 3];
+                            u[row] = p.foot_range[dd == 0 ? 0 : 2];
+                        } else { l[row] = 0; u[row] = 0; }
+                    }
+        }
+        for (int c = 0; c < NC; ++c)
+            for (int k = 0; k < N; ++k)
+                for (int r = 0; r < 5; ++r, ++row) {
+                    l[row] = -inf; u[row] = 0;
+                    if (lg[(size_t)k * NC + c] && r < 4) {
+                        const double *cs = &st[(size_t)k * SS + 32 + 32 * c];
+                        for (int qq = 0; qq < 3; ++qq) add(ui(k) + NUPC * c + FO + qq, cs[4 + 3 * r + qq]);
+                        u[row] = cs[16 + r];
+                    }
+                }
+        for (int k = 0; k < K1; ++k)
+            for (int j = 0; j < 8; ++j, ++row) {
+                for (int i = 0; i < 3; ++i) add(xi(k) + 6 + i, ((j >> i) & 1) ? -1.0 : 1.0);
+                add(ti(k), cw);
+                l[row] = -inf; u[row] = st[(size_t)k * SS + 18 + j];
+            }
+        for (int k = 0; k < K1; ++k, ++row) { add(ti(k), -1.0); l[row] = -inf; u[row] = 0; }
+        std::stable_sort(tr.begin(), tr.end(), [](auto &a, auto &c) {
+            return std::get<0>(a) != std::get<0>(c) ? std::get<0>(a) < std::get<0>(c) : std::get<1>(a) < std::get<1>(c);
+        });
+        int ci = 0;
+        for (size_t e = 0; e < tr.size(); ++e) {
+            while (ci <= std::get<0>(tr[e])) A_p[ci++] = (int)e;
+            A_x[e] = std::get<2>(tr[e]);
+            A_i[e] = std::get<1>(tr[e]);
+        }
+        while (ci <= n) A_p[ci++] = (int)tr.size();
+    });
+}
+
+int cmpc_get_qp_solution(cmpc_handle h, double *z, double *y, int32_t *status, int32_t *iters) {
+    return guard(h, [&] {
+        const int B = h->B, N = h->N, NC = h->NC, K1 = N + 1, NB = N + 2, NI = h->NI;
+        const int n = 9 * K1 + NU * N + K1 + N;
+        std::vector<double> xs, us, ts, nus, lams;
+        auto dl = [&](std::vector<double> &dst, void *src, size_t cnt) {
+            dst.resize(cnt);
+            if (h->prec == CMPC_PREC_F64) from_dev<double>(h, dst.data(), src, cnt); else from_dev<float>(h, dst.data(), src, cnt);
+        };
+        if (z) {
+            dl(xs, h->xs, (size_t)B * K1 * 9);
+            dl(us, h->us, (size_t)B * N * NU);
+            dl(ts, h->ts, (size_t)B * K1);
+            for (int b = 0; b < B; ++b) {
+                double *zb = z + (size_t)b * n;
+                std::memcpy(zb, &xs[(size_t)b * K1 * 9], sizeof(double) * K1 * 9);
+                std::memcpy(zb + 9 * K1, &us[(size_t)b * N * NU], sizeof(double) * N * NU);
+                std::memcpy(zb + 9 * K1 + NU * N, &ts[(size_t)b * K1], sizeof(double) * K1);
+                for (int k = 0; k < N; ++k) zb[9 * K1 + NU * N + K1 + k] = 0.0;
+            }
+        }
+        if (y) {
+            int32_t m = 0;
+            cmpc_qp_sizes(h, nullptr, &m, nullptr, nullptr);
+            dl(nus, h->nus, (size_t)B * NB * 9);
+            dl(lams, h->lams, (size_t)B * K1 * NI);
+            const int CP = 9 + 4 * NC;
+            for (int b = 0; b < B; ++b) {
+                double *yb = y + (size_t)b * m;
+                const double *nb = &nus[(size_t)b * NB * 9];
+                const double *lb = &lams[(size_t)b * K1 * NI];
+                int row = 0;
+                for (int i = 0; i < 9 * NB; ++i) {
+                    // nus blocks: init | dyn 0..N-1 | final  == rows init, dyn, final
+                    yb[row++] = nb[i];
+                }
+                if (h->robot == 1)
+                    for (int c = 0; c < NC; ++c)
+                        for (int dd = 0; dd < 2; ++dd)
+                            for (int k = 0; k < N; ++k)
+                                yb[row++] = lb[(size_t)k * NI + CP + 4 * c + 2 * dd] - lb[(size_t)k * NI + CP + 4 * c + 2 * dd + 1];
+                for (int c = 0; c < NC; ++c)
+                    for (int k = 0; k < N; ++k)
+                        for (int r = 0; r < 5; ++r) yb[row++] = r < 4 ? lb[(size_t)k * NI + 9 + 4 * c + r] : 0.0;
+                for (int k = 0; k < K1; ++k)
+                    for (int j = 0; j < 8; ++j) yb[row++] = lb[(size_t)k * NI + j];
+                for (int k = 0; k < K1; ++k) yb[row++] = lb[(size_t)k * NI + 8];
+            }
+        }
+        if (status) from_dev_raw(h, status, h->qp_status, (size_t)B * 4);
+        if (iters) from_dev_raw(h, iters, h->qp_iters, (size_t)B * 4);
+    });
+}
+
+int cmpc_get_solution(cmpc_handle h, double *X, double *U, double *K, double *Sigma, int32_t *n_accepted,
+                      int32_t *iterations, int32_t *scp_status, double *weight, double *radius) {
+    return guard(h, [&] {
+        const size_t B = h->B, N = h->N, K1 = N + 1;
+        auto dl = [&](double *dst, void *src, size_t n) {
+            if (h->prec == CMPC_PREC_F64) from_dev<double>(h, dst, src, n); else from_dev<float>(h, dst, src, n);
+        };
+        dl(X, h->Xacc, B * K1 * 9);
+        dl(U, h->Uacc, B * N * NU);
+        dl(K, h->Kacc, B * N * NU * 9);
+        dl(Sigma, h->Sacc, B * K1 * 81);
+        auto st = get_scp(h);
+        for (size_t b = 0; b < B; ++b) {
+            if (n_accepted) n_accepted[b] = st[b].n_accepted;
+            if (iterations) iterations[b] = st[b].iter;
+            if (scp_status) scp_status[b] = st[b].status;
+            if (weight) weight[b] = st[b].weight;
+            if (radius) radius[b] = st[b].radius;
+        }
+    });
+}
+
+int cmpc_get_iteration_log(cmpc_handle h, double *tr_norm, double *rho, int32_t *qp_status, int32_t *qp_iters,
+                           int32_t *decision) {
+    return guard(h, [&] {
+        auto st = get_scp(h);
+        for (int b = 0; b < h->B; ++b) {
+            if (tr_norm) tr_norm[b] = st[b].tr_norm;
+            if (rho) rho[b] = st[b].rho;
+            if (qp_status) qp_status[b] = st[b].qp_status;
+            if (qp_iters) qp_iters[b] = st[b].qp_iters;
+            if (decision) decision[b] = st[b].decision;
+        }
+    });
+}
+
+int cmpc_get_timing(cmpc_handle h, cmpc_timing *t) {
+    return guard(h, [&] {
+        need(t != nullptr, "null timing");
+        need(h->timed, "no timed iteration yet");
+        HIPCHK(hipEventSynchronize(h->ev[4]));
+        float ms[4];
+        for (int i = 0; i < 4; ++i) HIPCHK(hipEventElapsedTime(&ms[i], h->ev[i], h->ev[i + 1]));
+        t->linearize_ms = ms[0]; t->assemble_ms = ms[1]; t->qp_ms = ms[2]; t->accept_ms = ms[3];
+        HIPCHK(hipEventElapsedTime(&t->total_ms, h->ev[0], h->ev[4]));
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,144 @@
+// Shared definitions for the cmpc HIP kernels (gfx950 / CDNA4).
+//
+// Robot configurations are compile-time (template ROBOT): solo12 has 4 point contacts with
+// 3-D forces; TALOS has 2 contacts with u_i = [cop_x, cop_y, fx, fy, fz, tau_z]
+// (reference src/centroidal_model.py:189-212, src/optimizer.py:37-74).  nu = 12 for both.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "cmpc.h"
+
+namespace cmpc {
+
+constexpr int NX = 9;
+constexpr int NU = 12;
+constexpr int WAVE = 64;
+
+template <int ROBOT> struct Robot;
+template <> struct Robot<0> {             // solo12
+    static constexpr int NC = 4, NUPC = 3, FO = 0, COP = 0;
+};
+template <> struct Robot<1> {             // TALOS
+    static constexpr int NC = 2, NUPC = 6, FO = 2, COP = 1;
+};
+
+// Inequality rows per knot: TR L1 (8) | TR slack (1) | friction 4 per contact | CoP 4 per contact
+template <int ROBOT> struct Rows {
+    static constexpr int NC = Robot<ROBOT>::NC;
+    static constexpr int TR = 0, SL = 8, FR = 9, CP = 9 + 4 * NC;
+    static constexpr int NI = 9 + 4 * NC * (1 + Robot<ROBOT>::COP);   // 25 for both robots
+};
+
+// Stage record (assembled structured QP, one per knot), see assemble.hip.
+template <int ROBOT> struct Stage {
+    static constexpr int NC = Robot<ROBOT>::NC;
+    static constexpr int R = 0, QX = 9, BTR = 18, W = 26, CON = 32, CS = 32;
+    // per-contact slot offsets
+    static constexpr int ALPHA = 0, LEVER = 1, G = 4, H = 16, BCOP = 20, BTAU = 26;
+    static constexpr int SIZE = CON + CS * NC;
+};
+
+// Parameters of one problem class, in the compute type.
+template <typename T> struct DevParams {
+    T mass, gravity, dt, mu, xi;
+    T foot_range[4];
+    T Wx[9], Wu[12], Q[81], R[144], cov_w[144], cov_eta[81];
+    int stochastic, tracking;
+    double tr_radius0, omega0, omega_max, rho0, rho1, beta_succ, beta_fail, gamma_fail, conv_thr;
+    int max_iterations;
+};
+
+// Per-problem SCP state (always double: it mirrors the reference's Python floats).
+struct ScpState {
+    double weight, radius;
+    double tr_norm, rho;
+    int iter, status, success, n_accepted;
+    int qp_status, qp_iters, decision, active;
+};
+
+// Device buffers of one handle.
+template <typename T> struct DevBuf {
+    int B, N;
+    const int32_t *class_id;
+    const DevParams<T> *params;
+    const uint8_t *logic;    // (B,N,NC)
+    const T *pos, *rot;      // (B,N,NC,3) (B,N,NC,9)
+    const T *Xbar, *Ubar;    // (B,N+1,9) (B,N,NU)
+    // linearization
+    T *f, *A, *Bu, *C, *K, *Sig;    // (B,N,9) (B,N,81) (B,N,108) (B,N,9*3NC) (B,N,108) (B,N+1,81)
+    T *Acl, *Qw;                    // scan helpers (B,N,81) x2
+    // assembled stage records (B,N+1,SIZE) and per-problem cw = -1/omega
+    T *stage;
+    T *cw;
+    // QP solution / multipliers
+    T *xs, *us, *ts;                // (B,N+1,9) (B,N,NU) (B,N+1)
+    T *nus;                         // (B,N+2,9)
+    T *lams;                        // (B,N+1,NI)
+    int32_t *qp_status, *qp_iters;
+    // IPM workspace
+    T *ws;
+    size_t ws_stride;               // elements per problem
+    // SCP
+    ScpState *scp;
+    T *Xacc, *Uacc, *Kacc, *Sacc;   // accepted solution (B,N+1,9) (B,N,NU) (B,N,108) (B,N+1,81)
+};
+
+// ---------------------------------------------------------------- small helpers
+template <typename T> __device__ __forceinline__ T sq(T a) { return a * a; }
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <typename T> __device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    return v;
+}
+template <typename T> __device__ __forceinline__ T wave_min(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+    return v;
+}
+template <typename T> __device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Block-wide reductions for blockDim.x == NT (multiple of 64).  `red` is LDS scratch of
+// at least NT/64 * NV elements.  All threads receive the result.
+template <typename T, int NT, int NV, int OP>   // OP: 0 sum, 1 max, 2 min
+__device__ __forceinline__ void block_reduce(T (&v)[NV], T *red) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        T a = v[i];
+        a = OP == 0 ? wave_sum(a) : OP == 1 ? wave_max(a) : wave_min(a);
+        if (lane == 0) red[wid * NV + i] = a;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        T a = red[i];
+#pragma unroll
+        for (int w = 1; w < NT / 64; ++w) {
+            T b = red[w * NV + i];
+            a = OP == 0 ? a + b : OP == 1 ? fmax(a, b) : fmin(a, b);
+        }
+        v[i] = a;
+    }
+    __syncthreads();
+}
+
+// skew(v) * x  == v cross x
+template <typename T> __device__ __forceinline__ void cross3(const T *a, const T *b, T *o) {
+    o[0] = a[1] * b[2] - a[2] * b[1];
+    o[1] = a[2] * b[0] - a[0] * b[2];
+    o[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+}  // namespace cmpc

@@ -1,0 +1,922 @@
+// Batched structured interior-point QP (Mehrotra predictor-corrector) for the SCP subproblem.
+//
+// Replaces solve_subproblem (reference src/scp_solver.py:59-68: osqp.OSQP().setup(P, q, A, l,
+// u, eps_abs=1e-7, eps_rel=1e-7, polish=True).solve()).  Same QP, same unique minimizer; the
+// algorithm is chosen for the GPU: ~10-25 Newton steps instead of hundreds to thousands of
+// ADMM iterations, each step exploiting the stage structure ("QP").
+//
+// Newton system.  With Phi = H + G'DG (block diagonal per knot; the TR slack t_k is eliminated
+// inside its knot) the equality multipliers solve the dual Schur system S dnu = rhs with
+// S = E Phi^-1 E' block tridiagonal: N+2 blocks of 9x9 (init row, N dynamics rows, final
+// row).  Friction rows use the push-through form Phi^-1 G'D = W^-1 G'(D^-1 + G W^-1 G')^-1 so
+// no D * r product ever forms (D = lambda/s reaches 1e15+ near convergence).
+//
+// Mapping (one 256-thread workgroup per problem, all IPM iterations in one launch):
+//   thread k <-> knot k for every per-knot phase (residuals, Phi factors, S blocks, Newton
+//   back-substitution, step length); wave 0 runs the O(N) block-Cholesky of S and the two
+//   block sweeps per Newton solve with the 9x9 blocks staged in LDS.  Problems are
+//   independent, so the grid needs no inter-workgroup communication.
+#include "common.hpp"
+
+namespace cmpc {
+
+constexpr int NT = 256;
+constexpr int FU = 34;   // per-contact factor record: Gw 12 | Kinv 10 | F 6 | Winvd 6
+
+// Workspace offsets (elements) for one problem.
+struct WsLayout {
+    size_t s, l, x, u, t, nu, rdx, rdt, rdu, rde, rdi, facx, facu, Sd, So, wx, wt, wu, rhs, dnu, dx, dt, du,
+        ds, dl, dsa, dla, total;
+    __host__ __device__ WsLayout(int N, int NI, int NC) {
+        const size_t K1 = N + 1, NB = N + 2;
+        size_t o = 0;
+        auto take = [&](size_t n) { size_t r = o; o += (n + 7) & ~size_t(7); return r; };
+        s = take(K1 * NI); l = take(K1 * NI); x = take(K1 * 9); u = take(N * NU); t = take(K1);
+        nu = take(NB * 9); rdx = take(K1 * 9); rdt = take(K1); rdu = take(N * NU); rde = take(NB * 9);
+        rdi = take(K1 * NI); facx = take(K1 * 16); facu = take((size_t)N * NC * FU); Sd = take(NB * 81);
+        So = take((N + 1) * 81); wx = take(K1 * 9); wt = take(K1); wu = take(N * NU); rhs = take(NB * 9);
+        dnu = take(NB * 9); dx = take(K1 * 9); dt = take(K1); du = take(N * NU); ds = take(K1 * NI);
+        dl = take(K1 * NI); dsa = take(K1 * NI); dla = take(K1 * NI);
+        total = o;
+    }
+};
+
+template <typename T> __device__ __forceinline__ T tr_sign(int j, int i) { return ((j >> i) & 1) ? T(-1) : T(1); }
+
+// ------------------------------------------------------------------ compact A, B operators
+// A = [[I, beta I, 0], [0, I, 0], [[w]x, 0, I]] in (c, l, L) blocks.
+template <typename T> __device__ __forceinline__ void opA(const T *w, T beta, const T *x, T *o) {
+    for (int i = 0; i < 3; ++i) o[i] = x[i] + beta * x[3 + i];
+    for (int i = 0; i < 3; ++i) o[3 + i] = x[3 + i];
+    T wc[3];
+    cross3(w, x, wc);
+    for (int i = 0; i < 3; ++i) o[6 + i] = x[6 + i] + wc[i];
+}
+template <typename T> __device__ __forceinline__ void opAT(const T *w, T beta, const T *v, T *o) {
+    T vw[3];
+    cross3(v + 6, w, vw);   // [w]x' v_L = v_L x w
+    for (int i = 0; i < 3; ++i) o[i] = v[i] + vw[i];
+    for (int i = 0; i < 3; ++i) o[3 + i] = beta * v[i] + v[3 + i];
+    for (int i = 0; i < 3; ++i) o[6 + i] = v[6 + i];
+}
+template <typename T, int ROBOT> __device__ __forceinline__ void opB(const T *st, const T *u, T *o) {
+    constexpr int NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
+    using S = Stage<ROBOT>;
+    for (int i = 0; i < 9; ++i) o[i] = T(0);
+    for (int c = 0; c < NC; ++c) {
+        const T *cs = st + S::CON + S::CS * c;
+        const T a = cs[S::ALPHA];
+        const T *f = u + NUPC * c + FO;
+        T lf[3];
+        cross3(cs + S::LEVER, f, lf);
+        for (int i = 0; i < 3; ++i) { o[3 + i] += a * f[i]; o[6 + i] += a * lf[i]; }
+        if (ROBOT == 1) {
+            const T *cp = u + NUPC * c;
+            for (int r = 0; r < 3; ++r)
+                o[6 + r] += cs[S::BCOP + 2 * r] * cp[0] + cs[S::BCOP + 2 * r + 1] * cp[1] + cs[S::BTAU + r] * cp[5];
+        }
+    }
+}
+template <typename T, int ROBOT> __device__ __forceinline__ void opBT(const T *st, const T *v, T *o) {
+    constexpr int NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
+    using S = Stage<ROBOT>;
+    for (int c = 0; c < NC; ++c) {
+        const T *cs = st + S::CON + S::CS * c;
+        const T a = cs[S::ALPHA];
+        T vl[3];
+        cross3(v + 6, cs + S::LEVER, vl);   // [lev]x' v_L = v_L x lev
+        T *oc = o + NUPC * c;
+        for (int i = 0; i < 3; ++i) oc[FO + i] = a * (v[3 + i] + vl[i]);
+        if (ROBOT == 1) {
+            for (int q = 0; q < 2; ++q) {
+                T acc = T(0);
+                for (int r = 0; r < 3; ++r) acc += cs[S::BCOP + 2 * r + q] * v[6 + r];
+                oc[q] = acc;
+            }
+            oc[5] = cs[S::BTAU] * v[6] + cs[S::BTAU + 1] * v[7] + cs[S::BTAU + 2] * v[8];
+        }
+    }
+}
+
+// ------------------------------------------------------------------ per-problem context
+template <typename T, int ROBOT> struct Ctx {
+    static constexpr int NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
+    static constexpr int NI = Rows<ROBOT>::NI;
+    using R_ = Rows<ROBOT>;
+    using S = Stage<ROBOT>;
+    int N;
+    const DevParams<T> *prm;
+    const T *stage;       // (N+1, SIZE)
+    const uint8_t *logic; // (N, NC)
+    const T *xbar;        // (N+1, 9)
+    T cw, beta;
+    T *ws;
+    WsLayout L;
+
+    __device__ const T *st(int k) const { return stage + (size_t)k * S::SIZE; }
+    __device__ bool present(int k, int row) const {
+        if (row < R_::FR) return true;
+        if (k >= N) return false;
+        if (row < R_::CP) return logic[k * NC + (row - R_::FR) / 4] != 0;
+        return logic[k * NC + (row - R_::CP) / 4] != 0;
+    }
+    // g'z - h of row `row` at knot k for the knot-local (x, t, u)
+    __device__ T gz(int k, int row, const T *x, T t, const T *u, bool with_h) const {
+        if (row < 8) {
+            T v = tr_sign<T>(row, 0) * x[6] + tr_sign<T>(row, 1) * x[7] + tr_sign<T>(row, 2) * x[8] + cw * t;
+            return with_h ? v - st(k)[S::BTR + row] : v;
+        }
+        if (row == 8) return -t;
+        if (row < R_::CP) {
+            const int c = (row - R_::FR) / 4, r = (row - R_::FR) % 4;
+            const T *cs = st(k) + S::CON + S::CS * c;
+            const T *f = u + NUPC * c + FO;
+            T v = cs[S::G + 3 * r] * f[0] + cs[S::G + 3 * r + 1] * f[1] + cs[S::G + 3 * r + 2] * f[2];
+            return with_h ? v - cs[S::H + r] : v;
+        }
+        const int c = (row - R_::CP) / 4, dd = ((row - R_::CP) % 4) / 2, side = (row - R_::CP) % 2;
+        const T cop = u[NUPC * c + dd];
+        if (side == 0) {   // cop <= hi
+            return with_h ? cop - prm->foot_range[dd == 0 ? 0 : 2] : cop;
+        } else {           // -cop <= -lo, lo = -(lxn | lyn)
+            return with_h ? -cop - prm->foot_range[dd == 0 ? 1 : 3] : -cop;
+        }
+    }
+    // accumulate G' v of knot k into (gx (L part), gt, gu)
+    __device__ void gtv(int k, const T *v, T *gL, T &gt, T *gu) const {
+        gL[0] = gL[1] = gL[2] = T(0);
+        gt = T(0);
+        for (int j = 0; j < 8; ++j) {
+            for (int i = 0; i < 3; ++i) gL[i] += tr_sign<T>(j, i) * v[j];
+            gt += cw * v[j];
+        }
+        gt -= v[8];
+        if (k >= N) return;
+        for (int i = 0; i < NU; ++i) gu[i] = T(0);
+        for (int c = 0; c < NC; ++c) {
+            if (!logic[k * NC + c]) continue;
+            const T *cs = st(k) + S::CON + S::CS * c;
+            for (int r = 0; r < 4; ++r) {
+                const T vr = v[R_::FR + 4 * c + r];
+                for (int q = 0; q < 3; ++q) gu[NUPC * c + FO + q] += cs[S::G + 3 * r + q] * vr;
+            }
+            if (ROBOT == 1) {
+                for (int dd = 0; dd < 2; ++dd)
+                    gu[NUPC * c + dd] += v[R_::CP + 4 * c + 2 * dd] - v[R_::CP + 4 * c + 2 * dd + 1];
+            }
+        }
+    }
+    __device__ T *var_x(int k) const { return ws + L.x + (size_t)k * 9; }
+    __device__ T *var_u(int k) const { return ws + L.u + (size_t)k * NU; }
+};
+
+// 3x3 symmetric packed (00,10,11,20,21,22) helpers
+template <typename T> __device__ __forceinline__ T sym3(const T *p, int i, int j) {
+    if (i < j) { int t = i; i = j; j = t; }
+    return p[i * (i + 1) / 2 + j];
+}
+template <typename T> __device__ void inv3sym(const T (&a)[3][3], T *out) {
+    const T c00 = a[1][1] * a[2][2] - a[1][2] * a[2][1];
+    const T c01 = a[1][2] * a[2][0] - a[1][0] * a[2][2];
+    const T c02 = a[1][0] * a[2][1] - a[1][1] * a[2][0];
+    const T det = a[0][0] * c00 + a[0][1] * c01 + a[0][2] * c02;
+    const T id = T(1) / det;
+    const T c11 = a[0][0] * a[2][2] - a[0][2] * a[2][0];
+    const T c12 = a[0][2] * a[1][0] - a[0][0] * a[1][2];
+    const T c22 = a[0][0] * a[1][1] - a[0][1] * a[1][0];
+    out[0] = c00 * id; out[1] = c01 * id; out[2] = c11 * id;
+    out[3] = c02 * id; out[4] = c12 * id; out[5] = c22 * id;
+}
+// inverse of a 4x4 SPD matrix (Cholesky), packed symmetric (10 entries, row i col j<=i)
+template <typename T> __device__ void inv4spd(T (&a)[4][4], T *out) {
+    T Lm[4][4] = {};
+    for (int j = 0; j < 4; ++j) {
+        T d = a[j][j];
+        for (int q = 0; q < j; ++q) d -= Lm[j][q] * Lm[j][q];
+        d = sqrt(d);
+        Lm[j][j] = d;
+        for (int i = j + 1; i < 4; ++i) {
+            T v = a[i][j];
+            for (int q = 0; q < j; ++q) v -= Lm[i][q] * Lm[j][q];
+            Lm[i][j] = v / d;
+        }
+    }
+    T Li[4][4] = {};
+    for (int c = 0; c < 4; ++c) {
+        Li[c][c] = T(1) / Lm[c][c];
+        for (int i = c + 1; i < 4; ++i) {
+            T v = T(0);
+            for (int q = c; q < i; ++q) v += Lm[i][q] * Li[q][c];
+            Li[i][c] = -v / Lm[i][i];
+        }
+    }
+    int p = 0;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j <= i; ++j) {
+            T v = T(0);
+            for (int q = i; q < 4; ++q) v += Li[q][i] * Li[q][j];
+            out[p++] = v;
+        }
+}
+__device__ __forceinline__ int p4(int i, int j) { if (i < j) { int t = i; i = j; j = t; } return i * (i + 1) / 2 + j; }
+
+// ------------------------------------------------------------------ phases
+// (1) residuals of knot k; returns norm contributions
+template <typename T, int ROBOT> struct Norms { T prim, dual, comp, mu, sp, sd, lmax, cnt; };
+
+template <typename T, int ROBOT> __device__ void phase_residual(const Ctx<T, ROBOT> &C, int k, Norms<T, ROBOT> &nm) {
+    using S = Stage<ROBOT>;
+    constexpr int NI = Rows<ROBOT>::NI;
+    const int N = C.N;
+    const DevParams<T> &P = *C.prm;
+    const T *x = C.var_x(k);
+    const T t = C.ws[C.L.t + k];
+    const T *u = (k < N) ? C.var_u(k) : nullptr;
+    const T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
+    const T *nu = C.ws + C.L.nu;
+    T lv[NI];
+    for (int r = 0; r < NI; ++r) lv[r] = C.present(k, r) ? lm[r] : T(0);
+    T gL[3], gt, gu[NU];
+    C.gtv(k, lv, gL, gt, gu);
+    // E' nu at knot k
+    T ex[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (k == 0) for (int i = 0; i < 9; ++i) ex[i] += nu[i];
+    if (k < N) {
+        T a[9];
+        opAT(C.st(k) + S::W, C.beta, nu + (size_t)(1 + k) * 9, a);
+        for (int i = 0; i < 9; ++i) ex[i] += a[i];
+    }
+    if (k >= 1) for (int i = 0; i < 9; ++i) ex[i] -= nu[(size_t)k * 9 + i];
+    if (k == N) for (int i = 0; i < 9; ++i) ex[i] += nu[(size_t)(N + 1) * 9 + i];
+    const T *qx = C.st(k) + S::QX;
+    T *rdx = C.ws + C.L.rdx + (size_t)k * 9;
+    for (int i = 0; i < 9; ++i) {
+        const T hx = P.Wx[i] * x[i];
+        const T g = (i >= 6) ? gL[i - 6] : T(0);
+        rdx[i] = hx + qx[i] + ex[i] + g;
+        nm.dual = fmax(nm.dual, fabs(rdx[i]));
+        nm.sd = fmax(nm.sd, fmax(fabs(hx), fmax(fabs(qx[i]), fmax(fabs(ex[i]), fabs(g)))));
+    }
+    const T rdt = T(1) + gt;
+    C.ws[C.L.rdt + k] = rdt;
+    nm.dual = fmax(nm.dual, fabs(rdt));
+    nm.sd = fmax(nm.sd, T(1));
+    if (k < N) {
+        T eu[NU];
+        opBT<T, ROBOT>(C.st(k), nu + (size_t)(1 + k) * 9, eu);
+        T *rdu = C.ws + C.L.rdu + (size_t)k * NU;
+        for (int i = 0; i < NU; ++i) {
+            const T hu = P.Wu[i] * u[i];
+            rdu[i] = hu + eu[i] + gu[i];
+            nm.dual = fmax(nm.dual, fabs(rdu[i]));
+            nm.sd = fmax(nm.sd, fmax(fabs(hu), fmax(fabs(eu[i]), fabs(gu[i]))));
+        }
+        // dynamics row block 1+k
+        T ax[9], bu[9];
+        opA(C.st(k) + S::W, C.beta, x, ax);
+        opB<T, ROBOT>(C.st(k), u, bu);
+        const T *x1 = C.var_x(k + 1);
+        const T *r = C.st(k) + S::R;
+        T *rde = C.ws + C.L.rde + (size_t)(1 + k) * 9;
+        for (int i = 0; i < 9; ++i) {
+            const T ez = ax[i] + bu[i] - x1[i];
+            rde[i] = ez - r[i];
+            nm.prim = fmax(nm.prim, fabs(rde[i]));
+            nm.sp = fmax(nm.sp, fmax(fabs(ez), fabs(r[i])));
+        }
+    }
+    if (k == 0 || k == N) {
+        const int blk = (k == 0) ? 0 : N + 1;
+        T *rde = C.ws + C.L.rde + (size_t)blk * 9;
+        const T *xb = C.xbar + (size_t)k * 9;
+        for (int i = 0; i < 9; ++i) {
+            rde[i] = x[i] - xb[i];
+            nm.prim = fmax(nm.prim, fabs(rde[i]));
+            nm.sp = fmax(nm.sp, fmax(fabs(x[i]), fabs(xb[i])));
+        }
+    }
+    T *rdi = C.ws + C.L.rdi + (size_t)k * NI;
+    for (int r = 0; r < NI; ++r) {
+        if (!C.present(k, r)) { rdi[r] = T(0); continue; }
+        const T g = C.gz(k, r, x, t, u, false);
+        const T v = C.gz(k, r, x, t, u, true);
+        rdi[r] = v + s[r];
+        nm.prim = fmax(nm.prim, fmax(v, T(0)));
+        nm.sp = fmax(nm.sp, fmax(fabs(g), fabs(g - v)));
+        const T c = s[r] * lm[r];
+        nm.comp = fmax(nm.comp, c);
+        nm.mu += c;
+        nm.cnt += T(1);
+        nm.lmax = fmax(nm.lmax, lm[r]);
+    }
+}
+
+// (2) Phi factors of knot k
+template <typename T, int ROBOT> __device__ void phase_factor(const Ctx<T, ROBOT> &C, int k) {
+    using S = Stage<ROBOT>;
+    using R_ = Rows<ROBOT>;
+    constexpr int NI = R_::NI, NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
+    const int N = C.N;
+    const DevParams<T> &P = *C.prm;
+    const T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
+    T *fx = C.ws + C.L.facx + (size_t)k * 16;
+    T D[9];
+    for (int r = 0; r < 9; ++r) D[r] = lm[r] / s[r];
+    T A3[3][3], Lt[3] = {0, 0, 0}, tt = D[8];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) A3[i][j] = (i == j) ? P.Wx[6 + i] : T(0);
+    for (int j = 0; j < 8; ++j) {
+        for (int i = 0; i < 3; ++i) {
+            Lt[i] += C.cw * D[j] * tr_sign<T>(j, i);
+            for (int q = 0; q < 3; ++q) A3[i][q] += D[j] * tr_sign<T>(j, i) * tr_sign<T>(j, q);
+        }
+        tt += C.cw * C.cw * D[j];
+    }
+    for (int i = 0; i < 3; ++i)
+        for (int q = 0; q < 3; ++q) A3[i][q] -= Lt[i] * Lt[q] / tt;
+    for (int i = 0; i < 6; ++i) fx[i] = T(1) / P.Wx[i];
+    inv3sym(A3, fx + 6);
+    fx[12] = Lt[0]; fx[13] = Lt[1]; fx[14] = Lt[2]; fx[15] = tt;
+    if (k >= N) return;
+    for (int c = 0; c < NC; ++c) {
+        T *fu = C.ws + C.L.facu + ((size_t)k * NC + c) * FU;
+        const T *Wc = P.Wu + NUPC * c;
+        // Winvd: inverse diagonal of W' (CoP rows fold into their coordinate's diagonal)
+        for (int q = 0; q < NUPC; ++q) fu[28 + q] = T(1) / Wc[q];
+        if (ROBOT == 1 && C.logic[k * NC + c]) {
+            for (int dd = 0; dd < 2; ++dd) {
+                const int r0 = R_::CP + 4 * c + 2 * dd;
+                fu[28 + dd] = T(1) / (Wc[dd] + lm[r0] / s[r0] + lm[r0 + 1] / s[r0 + 1]);
+            }
+        }
+        const T wi[3] = {T(1) / Wc[FO], T(1) / Wc[FO + 1], T(1) / Wc[FO + 2]};
+        if (!C.logic[k * NC + c]) {
+            for (int q = 0; q < 12; ++q) fu[q] = T(0);
+            for (int q = 0; q < 10; ++q) fu[12 + q] = T(0);
+            fu[12 + 0] = fu[12 + 2] = fu[12 + 5] = fu[12 + 9] = T(1);
+            fu[22] = wi[0]; fu[23] = T(0); fu[24] = wi[1]; fu[25] = T(0); fu[26] = T(0); fu[27] = wi[2];
+            continue;
+        }
+        const T *cs = C.st(k) + S::CON + S::CS * c;
+        T Gw[4][3];
+        for (int r = 0; r < 4; ++r)
+            for (int q = 0; q < 3; ++q) { Gw[r][q] = cs[S::G + 3 * r + q] * wi[q]; fu[3 * r + q] = Gw[r][q]; }
+        T Km[4][4];
+        for (int r = 0; r < 4; ++r)
+            for (int q = 0; q < 4; ++q) {
+                T acc = (r == q) ? s[R_::FR + 4 * c + r] / lm[R_::FR + 4 * c + r] : T(0);
+                for (int z = 0; z < 3; ++z) acc += Gw[r][z] * cs[S::G + 3 * q + z];
+                Km[r][q] = acc;
+            }
+        T Ki[10];
+        inv4spd(Km, Ki);
+        for (int q = 0; q < 10; ++q) fu[12 + q] = Ki[q];
+        // F = W^-1 - Gw' Kinv Gw
+        int p = 0;
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j <= i; ++j) {
+                T acc = (i == j) ? wi[i] : T(0);
+                for (int r = 0; r < 4; ++r)
+                    for (int q = 0; q < 4; ++q) acc -= Gw[r][i] * Ki[p4(r, q)] * Gw[q][j];
+                fu[22 + p++] = acc;
+            }
+    }
+}
+
+// Phi^-1 v for knot k: (vx[9], vt, vu[NU]) -> (ox, ot, ou)
+template <typename T, int ROBOT>
+__device__ void phi_solve(const Ctx<T, ROBOT> &C, int k, const T *vx, T vt, const T *vu, T *ox, T &ot, T *ou) {
+    constexpr int NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
+    const T *fx = C.ws + C.L.facx + (size_t)k * 16;
+    const T tt = fx[15];
+    T w[3];
+    for (int i = 0; i < 3; ++i) w[i] = vx[6 + i] - fx[12 + i] * (vt / tt);
+    for (int i = 0; i < 6; ++i) ox[i] = fx[i] * vx[i];
+    for (int i = 0; i < 3; ++i) ox[6 + i] = sym3(fx + 6, i, 0) * w[0] + sym3(fx + 6, i, 1) * w[1] + sym3(fx + 6, i, 2) * w[2];
+    ot = (vt - (fx[12] * ox[6] + fx[13] * ox[7] + fx[14] * ox[8])) / tt;
+    if (k >= C.N) return;
+    for (int c = 0; c < NC; ++c) {
+        const T *fu = C.ws + C.L.facu + ((size_t)k * NC + c) * FU;
+        const T *vc = vu + NUPC * c;
+        T *oc = ou + NUPC * c;
+        for (int q = 0; q < NUPC; ++q) oc[q] = fu[28 + q] * vc[q];
+        for (int i = 0; i < 3; ++i)
+            oc[FO + i] = sym3(fu + 22, i, 0) * vc[FO] + sym3(fu + 22, i, 1) * vc[FO + 1] + sym3(fu + 22, i, 2) * vc[FO + 2];
+    }
+}
+
+// (3) S blocks owned by knot k
+template <typename T, int ROBOT> __device__ void phase_sblock(const Ctx<T, ROBOT> &C, int k) {
+    using S = Stage<ROBOT>;
+    constexpr int NC = Robot<ROBOT>::NC;
+    const int N = C.N;
+    const T beta = C.beta;
+    const T *fx = C.ws + C.L.facx + (size_t)k * 16;
+    auto Mfull = [&](const T *f, int i, int j) -> T {   // M_k entry
+        if (i < 6 || j < 6) return (i == j && i < 6) ? f[i] : T(0);
+        return sym3(f + 6, i - 6, j - 6);
+    };
+    // M A' blocks:  [[Mc, 0, Mc W'], [beta Ml, Ml, 0], [0, 0, ML]]
+    auto MAt = [&](const T *f, const T *w, int i, int j) -> T {
+        const T Wm[3][3] = {{0, -w[2], w[1]}, {w[2], 0, -w[0]}, {-w[1], w[0], 0}};
+        if (i < 3) {
+            if (j < 3) return (i == j) ? f[i] : T(0);
+            if (j < 6) return T(0);
+            return f[i] * Wm[j - 6][i];
+        }
+        if (i < 6) {
+            if (j < 3) return (i - 3 == j) ? beta * f[i] : T(0);
+            if (j < 6) return (i == j) ? f[i] : T(0);
+            return T(0);
+        }
+        if (j < 6) return T(0);
+        return sym3(f + 6, i - 6, j - 6);
+    };
+    if (k == 0) {
+        T *Sd = C.ws + C.L.Sd, *So = C.ws + C.L.So;
+        for (int i = 0; i < 9; ++i)
+            for (int j = 0; j < 9; ++j) {
+                Sd[i * 9 + j] = Mfull(fx, i, j);
+                So[i * 9 + j] = MAt(fx, C.st(0) + S::W, i, j);
+            }
+    }
+    if (k == N) {
+        T *Sd = C.ws + C.L.Sd + (size_t)(N + 1) * 81;
+        for (int i = 0; i < 9; ++i)
+            for (int j = 0; j < 9; ++j) Sd[i * 9 + j] = Mfull(fx, i, j);
+        return;
+    }
+    const T *fx1 = fx + 16;
+    const T *w = C.st(k) + S::W;
+    const T Wm[3][3] = {{0, -w[2], w[1]}, {w[2], 0, -w[0]}, {-w[1], w[0], 0}};
+    T Sm[9][9];
+    // A M A'
+    for (int i = 0; i < 9; ++i)
+        for (int j = 0; j < 9; ++j) Sm[i][j] = T(0);
+    const T *mc = fx, *ml = fx + 3;
+    for (int a = 0; a < 3; ++a) {
+        Sm[a][a] = mc[a] + beta * beta * ml[a];
+        Sm[a][3 + a] = Sm[3 + a][a] = beta * ml[a];
+        Sm[3 + a][3 + a] = ml[a];
+    }
+    for (int a = 0; a < 3; ++a)
+        for (int bb = 0; bb < 3; ++bb) {
+            Sm[a][6 + bb] = mc[a] * Wm[bb][a];   // Mc W'
+            Sm[6 + bb][a] = Sm[a][6 + bb];
+            T acc = sym3(fx + 6, a, bb);
+            for (int q = 0; q < 3; ++q) acc += Wm[a][q] * mc[q] * Wm[bb][q];
+            Sm[6 + a][6 + bb] = acc;
+        }
+    // B Phi_u^-1 B'
+    for (int c = 0; c < NC; ++c) {
+        const T *cs = C.st(k) + S::CON + S::CS * c;
+        const T al = cs[S::ALPHA];
+        if (al == T(0)) continue;
+        const T *fu = C.ws + C.L.facu + ((size_t)k * NC + c) * FU;
+        const T *lv = cs + S::LEVER;
+        const T Lm[3][3] = {{0, -lv[2], lv[1]}, {lv[2], 0, -lv[0]}, {-lv[1], lv[0], 0}};
+        T F[3][3], FL[3][3];   // F, F Lambda'
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) F[i][j] = sym3(fu + 22, i, j);
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) FL[i][j] = F[i][0] * Lm[j][0] + F[i][1] * Lm[j][1] + F[i][2] * Lm[j][2];
+        const T a2 = al * al;
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) {
+                Sm[3 + i][3 + j] += a2 * F[i][j];
+                Sm[3 + i][6 + j] += a2 * FL[i][j];
+                Sm[6 + j][3 + i] += a2 * FL[i][j];
+                T acc = T(0);
+                for (int q = 0; q < 3; ++q) acc += Lm[i][q] * FL[q][j];
+                Sm[6 + i][6 + j] += a2 * acc;
+            }
+        if (ROBOT == 1) {
+            const T *bc = cs + S::BCOP, *bt = cs + S::BTAU;
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j)
+                    Sm[6 + i][6 + j] += bc[2 * i] * fu[28] * bc[2 * j] + bc[2 * i + 1] * fu[29] * bc[2 * j + 1] +
+                                        bt[i] * fu[33] * bt[j];
+        }
+    }
+    // + M_{k+1}
+    for (int i = 0; i < 9; ++i)
+        for (int j = 0; j < 9; ++j) Sm[i][j] += Mfull(fx1, i, j);
+    T *Sd = C.ws + C.L.Sd + (size_t)(1 + k) * 81;
+    for (int e = 0; e < 81; ++e) Sd[e] = Sm[e / 9][e % 9];
+    T *So = C.ws + C.L.So + (size_t)(1 + k) * 81;
+    if (k + 1 < N) {
+        const T *w1 = C.st(k + 1) + S::W;
+        for (int i = 0; i < 9; ++i)
+            for (int j = 0; j < 9; ++j) So[i * 9 + j] = -MAt(fx1, w1, i, j);
+    } else {
+        for (int i = 0; i < 9; ++i)
+            for (int j = 0; j < 9; ++j) So[i * 9 + j] = -Mfull(fx1, i, j);
+    }
+}
+
+// (4) block Cholesky of S (wave 0).  Sd[j] <- Lc_j^-1 (lower), So[j] <- Lo_j = S_{j,j+1}' Lc_j^-T
+template <typename T> __device__ void seq_factor(T *Sd, T *So, int NB, T *sh) {
+    const int lane = threadIdx.x & 63;
+    T *Lm = sh, *Li = sh + 81, *Lp = sh + 162;   // working block, its inverse, previous Lo
+    for (int j = 0; j < NB; ++j) {
+        const T *Sj = Sd + (size_t)j * 81;
+        for (int e = lane; e < 81; e += WAVE) {
+            const int i = e / 9, c = e % 9;
+            T v = Sj[e];
+            if (j > 0 && c <= i)
+                for (int m = 0; m < 9; ++m) v -= Lp[i * 9 + m] * Lp[c * 9 + m];
+            Lm[e] = v;
+        }
+        wave_sync();
+        // Cholesky (lower) in Lm
+        for (int c = 0; c < 9; ++c) {
+            const T d = sqrt(Lm[c * 9 + c]);
+            const T id = T(1) / d;
+            wave_sync();
+            if (lane > c && lane < 9) Lm[lane * 9 + c] *= id;
+            if (lane == c) Lm[c * 9 + c] = d;
+            wave_sync();
+            for (int e = lane; e < 81; e += WAVE) {
+                const int i = e / 9, q = e % 9;
+                if (q > c && i >= q) Lm[e] -= Lm[i * 9 + c] * Lm[q * 9 + c];
+            }
+            wave_sync();
+        }
+        // inverse of the lower factor, lane = column
+        if (lane < 9) {
+            const int c = lane;
+            for (int i = 0; i < 9; ++i) Li[i * 9 + c] = T(0);
+            Li[c * 9 + c] = T(1) / Lm[c * 9 + c];
+            for (int i = c + 1; i < 9; ++i) {
+                T v = T(0);
+                for (int q = c; q < i; ++q) v += Lm[i * 9 + q] * Li[q * 9 + c];
+                Li[i * 9 + c] = -v / Lm[i * 9 + i];
+            }
+        }
+        wave_sync();
+        T *Dj = Sd + (size_t)j * 81;
+        for (int e = lane; e < 81; e += WAVE) Dj[e] = Li[e];
+        if (j + 1 < NB) {
+            const T *Oj = So + (size_t)j * 81;
+            T out[2];
+            for (int r = 0, e = lane; e < 81; e += WAVE, ++r) {   // Lo[i][c] = sum_m So[m][i] Li[c][m]
+                const int i = e / 9, c = e % 9;
+                T v = T(0);
+                for (int m = 0; m <= c; ++m) v += Oj[m * 9 + i] * Li[c * 9 + m];
+                out[r] = v;
+            }
+            wave_sync();
+            T *Oo = So + (size_t)j * 81;
+            for (int r = 0, e = lane; e < 81; e += WAVE, ++r) { Lp[e] = out[r]; Oo[e] = out[r]; }
+        }
+        wave_sync();
+    }
+}
+
+// (5c) forward / backward block sweeps: rhs -> dnu
+template <typename T> __device__ void seq_solve(const T *Li, const T *Lo, T *rhs, T *dnu, int NB, T *sh) {
+    const int lane = threadIdx.x & 63;
+    T *yp = sh, *tv = sh + 16;
+    if (lane < 9) yp[lane] = T(0);
+    wave_sync();
+    for (int j = 0; j < NB; ++j) {
+        if (lane < 9) {
+            T v = rhs[(size_t)j * 9 + lane];
+            if (j > 0) {
+                const T *O = Lo + (size_t)(j - 1) * 81 + lane * 9;
+                for (int m = 0; m < 9; ++m) v -= O[m] * yp[m];
+            }
+            tv[lane] = v;
+        }
+        wave_sync();
+        if (lane < 9) {
+            const T *Lj = Li + (size_t)j * 81 + lane * 9;
+            T v = T(0);
+            for (int m = 0; m <= lane; ++m) v += Lj[m] * tv[m];
+            rhs[(size_t)j * 9 + lane] = v;
+            yp[lane] = v;
+        }
+        wave_sync();
+    }
+    if (lane < 9) yp[lane] = T(0);
+    wave_sync();
+    for (int j = NB - 1; j >= 0; --j) {
+        if (lane < 9) {
+            T v = rhs[(size_t)j * 9 + lane];
+            if (j < NB - 1) {
+                const T *O = Lo + (size_t)j * 81;
+                for (int m = 0; m < 9; ++m) v -= O[m * 9 + lane] * yp[m];
+            }
+            tv[lane] = v;
+        }
+        wave_sync();
+        if (lane < 9) {
+            const T *Lj = Li + (size_t)j * 81;
+            T v = T(0);
+            for (int m = lane; m < 9; ++m) v += Lj[m * 9 + lane] * tv[m];
+            dnu[(size_t)j * 9 + lane] = v;
+            yp[lane] = v;
+        }
+        wave_sync();
+    }
+}
+
+// r_hat = r_i - r_c / lambda for the rows of knot k  (rc supplied per mode)
+template <typename T, int ROBOT>
+__device__ void rhat_rows(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu, T *rh) {
+    constexpr int NI = Rows<ROBOT>::NI;
+    const T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
+    const T *rdi = C.ws + C.L.rdi + (size_t)k * NI;
+    const T *dsa = C.ws + C.L.dsa + (size_t)k * NI, *dla = C.ws + C.L.dla + (size_t)k * NI;
+    for (int r = 0; r < NI; ++r) {
+        if (!C.present(k, r)) { rh[r] = T(0); continue; }
+        T rc = s[r] * lm[r];
+        if (corr) rc += dsa[r] * dla[r] - sigma_mu;
+        rh[r] = rdi[r] - rc / lm[r];
+    }
+}
+
+// (5a) particular solution w = Phi^-1 (r_d + G' D rhat) (friction rows in push-through form)
+template <typename T, int ROBOT> __device__ void phase_w(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu) {
+    using R_ = Rows<ROBOT>;
+    constexpr int NI = R_::NI, NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
+    const int N = C.N;
+    const T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
+    T rh[NI], v[NI];
+    rhat_rows(C, k, corr, sigma_mu, rh);
+    for (int r = 0; r < NI; ++r) v[r] = (r < R_::FR || r >= R_::CP) ? (lm[r] / s[r]) * rh[r] : T(0);
+    T gL[3], gt, gu[NU];
+    C.gtv(k, v, gL, gt, gu);
+    T vx[9], vu[NU];
+    const T *rdx = C.ws + C.L.rdx + (size_t)k * 9;
+    for (int i = 0; i < 9; ++i) vx[i] = rdx[i] + (i >= 6 ? gL[i - 6] : T(0));
+    const T vt = C.ws[C.L.rdt + k] + gt;
+    if (k < N) {
+        const T *rdu = C.ws + C.L.rdu + (size_t)k * NU;
+        for (int i = 0; i < NU; ++i) vu[i] = rdu[i] + gu[i];
+    }
+    T ox[9], ot, ou[NU];
+    phi_solve(C, k, vx, vt, vu, ox, ot, ou);
+    T *wx = C.ws + C.L.wx + (size_t)k * 9;
+    for (int i = 0; i < 9; ++i) wx[i] = ox[i];
+    C.ws[C.L.wt + k] = ot;
+    if (k < N) {
+        for (int c = 0; c < NC; ++c) {
+            if (!C.logic[k * NC + c]) continue;
+            const T *fu = C.ws + C.L.facu + ((size_t)k * NC + c) * FU;
+            T kr[4];
+            for (int r = 0; r < 4; ++r) {
+                T acc = T(0);
+                for (int q = 0; q < 4; ++q) acc += fu[12 + p4(r, q)] * rh[R_::FR + 4 * c + q];
+                kr[r] = acc;
+            }
+            for (int i = 0; i < 3; ++i) {
+                T acc = T(0);
+                for (int r = 0; r < 4; ++r) acc += fu[3 * r + i] * kr[r];
+                ou[NUPC * c + FO + i] += acc;
+            }
+        }
+        T *wu = C.ws + C.L.wu + (size_t)k * NU;
+        for (int i = 0; i < NU; ++i) wu[i] = ou[i];
+    }
+}
+
+// (5b) Schur right-hand side blocks owned by knot k: rhs = r_e - E w
+template <typename T, int ROBOT> __device__ void phase_rhs(const Ctx<T, ROBOT> &C, int k) {
+    using S = Stage<ROBOT>;
+    const int N = C.N;
+    const T *wx = C.ws + C.L.wx + (size_t)k * 9;
+    const T *rde = C.ws + C.L.rde;
+    T *rhs = C.ws + C.L.rhs;
+    if (k == 0) for (int i = 0; i < 9; ++i) rhs[i] = rde[i] - wx[i];
+    if (k == N) for (int i = 0; i < 9; ++i) rhs[(size_t)(N + 1) * 9 + i] = rde[(size_t)(N + 1) * 9 + i] - wx[i];
+    if (k < N) {
+        T ax[9], bu[9];
+        opA(C.st(k) + S::W, C.beta, wx, ax);
+        opB<T, ROBOT>(C.st(k), C.ws + C.L.wu + (size_t)k * NU, bu);
+        const T *wx1 = wx + 9;
+        for (int i = 0; i < 9; ++i)
+            rhs[(size_t)(1 + k) * 9 + i] = rde[(size_t)(1 + k) * 9 + i] - (ax[i] + bu[i] - wx1[i]);
+    }
+}
+
+// (5d) direction at knot k from dnu; returns the max step allowed by this knot's rows
+template <typename T, int ROBOT>
+__device__ T phase_dz(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu) {
+    using S = Stage<ROBOT>;
+    using R_ = Rows<ROBOT>;
+    constexpr int NI = R_::NI, NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
+    const int N = C.N;
+    const T *dnu = C.ws + C.L.dnu;
+    T ex[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, eu[NU];
+    if (k == 0) for (int i = 0; i < 9; ++i) ex[i] += dnu[i];
+    if (k < N) {
+        T a[9];
+        opAT(C.st(k) + S::W, C.beta, dnu + (size_t)(1 + k) * 9, a);
+        for (int i = 0; i < 9; ++i) ex[i] += a[i];
+        opBT<T, ROBOT>(C.st(k), dnu + (size_t)(1 + k) * 9, eu);
+    }
+    if (k >= 1) for (int i = 0; i < 9; ++i) ex[i] -= dnu[(size_t)k * 9 + i];
+    if (k == N) for (int i = 0; i < 9; ++i) ex[i] += dnu[(size_t)(N + 1) * 9 + i];
+    T ax[9], at, au[NU];
+    phi_solve(C, k, ex, T(0), eu, ax, at, au);
+    T dx[9], dtt, du[NU];
+    const T *wx = C.ws + C.L.wx + (size_t)k * 9, *wu = C.ws + C.L.wu + (size_t)k * NU;
+    for (int i = 0; i < 9; ++i) dx[i] = -wx[i] - ax[i];
+    dtt = -C.ws[C.L.wt + k] - at;
+    if (k < N) for (int i = 0; i < NU; ++i) du[i] = -wu[i] - au[i];
+    T *gdx = C.ws + C.L.dx + (size_t)k * 9;
+    for (int i = 0; i < 9; ++i) gdx[i] = dx[i];
+    C.ws[C.L.dt + k] = dtt;
+    if (k < N) { T *gdu = C.ws + C.L.du + (size_t)k * NU; for (int i = 0; i < NU; ++i) gdu[i] = du[i]; }
+    // rows
+    const T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
+    const T *rdi = C.ws + C.L.rdi + (size_t)k * NI;
+    T rh[NI];
+    rhat_rows(C, k, corr, sigma_mu, rh);
+    T *ds = C.ws + (corr ? C.L.ds : C.L.dsa) + (size_t)k * NI;
+    T *dl = C.ws + (corr ? C.L.dl : C.L.dla) + (size_t)k * NI;
+    T amax = T(1);
+    for (int r = 0; r < NI; ++r) {
+        if (!C.present(k, r)) { ds[r] = T(0); dl[r] = T(0); continue; }
+        const T g = C.gz(k, r, dx, dtt, du, false);
+        ds[r] = -rdi[r] - g;
+        if (r < R_::FR || r >= R_::CP) dl[r] = (lm[r] / s[r]) * (g + rh[r]);
+    }
+    if (k < N) {
+        // friction: dlam = Kinv (Gw v + rhat),  v = -(rdu + E'dnu_u) restricted to f
+        const T *rdu = C.ws + C.L.rdu + (size_t)k * NU;
+        for (int c = 0; c < NC; ++c) {
+            if (!C.logic[k * NC + c]) continue;
+            const T *fu = C.ws + C.L.facu + ((size_t)k * NC + c) * FU;
+            T vf[3];
+            for (int i = 0; i < 3; ++i) vf[i] = -(rdu[NUPC * c + FO + i] + eu[NUPC * c + FO + i]);
+            T z[4];
+            for (int r = 0; r < 4; ++r) z[r] = fu[3 * r] * vf[0] + fu[3 * r + 1] * vf[1] + fu[3 * r + 2] * vf[2] + rh[R_::FR + 4 * c + r];
+            for (int r = 0; r < 4; ++r) {
+                T acc = T(0);
+                for (int q = 0; q < 4; ++q) acc += fu[12 + p4(r, q)] * z[q];
+                dl[R_::FR + 4 * c + r] = acc;
+            }
+        }
+    }
+    for (int r = 0; r < NI; ++r) {
+        if (!C.present(k, r)) continue;
+        if (ds[r] < T(0)) amax = fmin(amax, -s[r] / ds[r]);
+        if (dl[r] < T(0)) amax = fmin(amax, -lm[r] / dl[r]);
+    }
+    return amax;
+}
+
+template <typename T, int ROBOT> __device__ T mu_after(const Ctx<T, ROBOT> &C, int k, T a) {
+    constexpr int NI = Rows<ROBOT>::NI;
+    const T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
+    const T *ds = C.ws + C.L.dsa + (size_t)k * NI, *dl = C.ws + C.L.dla + (size_t)k * NI;
+    T acc = T(0);
+    for (int r = 0; r < NI; ++r)
+        if (C.present(k, r)) acc += (s[r] + a * ds[r]) * (lm[r] + a * dl[r]);
+    return acc;
+}
+
+template <typename T, int ROBOT> __device__ void phase_update(const Ctx<T, ROBOT> &C, int k, T a) {
+    constexpr int NI = Rows<ROBOT>::NI;
+    const int N = C.N;
+    T *x = C.var_x(k);
+    const T *dx = C.ws + C.L.dx + (size_t)k * 9;
+    for (int i = 0; i < 9; ++i) x[i] += a * dx[i];
+    C.ws[C.L.t + k] += a * C.ws[C.L.dt + k];
+    if (k < N) {
+        T *u = C.var_u(k);
+        const T *du = C.ws + C.L.du + (size_t)k * NU;
+        for (int i = 0; i < NU; ++i) u[i] += a * du[i];
+    }
+    T *nu = C.ws + C.L.nu;
+    const T *dnu = C.ws + C.L.dnu;
+    for (int i = 0; i < 9; ++i) nu[(size_t)(1 + k) * 9 + i] += a * dnu[(size_t)(1 + k) * 9 + i];   // k<N: dyn k; k==N: final
+    if (k == 0) for (int i = 0; i < 9; ++i) nu[i] += a * dnu[i];
+    T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
+    const T *ds = C.ws + C.L.ds + (size_t)k * NI, *dl = C.ws + C.L.dl + (size_t)k * NI;
+    for (int r = 0; r < NI; ++r) {
+        if (!C.present(k, r)) continue;
+        s[r] += a * ds[r];
+        lm[r] += a * dl[r];
+    }
+}
+
+// ------------------------------------------------------------------ kernel
+template <typename T, int ROBOT>
+__global__ void __launch_bounds__(NT) k_qp_ipm(DevBuf<T> d, int only_active, int max_iter, T eps_abs, T eps_rel,
+                                               T eta) {
+    constexpr int NI = Rows<ROBOT>::NI;
+    const int b = blockIdx.x;
+    if (b >= d.B) return;
+    if (only_active && !d.scp[b].active) return;
+    __shared__ T red[8 * (NT / 64)];
+    __shared__ T sh[256];
+    const int tid = threadIdx.x, N = d.N, K1 = N + 1, NB = N + 2;
+    Ctx<T, ROBOT> C{N, nullptr, nullptr, nullptr, nullptr, T(0), T(0), nullptr, WsLayout(N, NI, Robot<ROBOT>::NC)};
+    C.prm = d.params + d.class_id[b];
+    C.stage = d.stage + (size_t)b * K1 * Stage<ROBOT>::SIZE;
+    C.logic = d.logic + (size_t)b * N * Robot<ROBOT>::NC;
+    C.xbar = d.Xbar + (size_t)b * K1 * 9;
+    C.cw = d.cw[b];
+    C.beta = C.prm->dt / C.prm->mass;
+    C.ws = d.ws + (size_t)b * d.ws_stride;
+    // ---- initial point: z = (xbar, ubar, 0), nu = 0, s = max(h - gz, 1), lambda = 1
+    for (int k = tid; k < K1; k += NT) {
+        T *x = C.var_x(k);
+        for (int i = 0; i < 9; ++i) x[i] = C.xbar[(size_t)k * 9 + i];
+        C.ws[C.L.t + k] = T(0);
+        const T *ubar = d.Ubar + ((size_t)b * N + (k < N ? k : 0)) * NU;
+        if (k < N) { T *u = C.var_u(k); for (int i = 0; i < NU; ++i) u[i] = ubar[i]; }
+        T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
+        for (int r = 0; r < NI; ++r) {
+            if (C.present(k, r)) {
+                s[r] = fmax(-C.gz(k, r, x, T(0), k < N ? ubar : nullptr, true), T(1));
+                lm[r] = T(1);
+            } else { s[r] = T(1); lm[r] = T(0); }
+        }
+        T *dsa = C.ws + C.L.dsa + (size_t)k * NI, *dla = C.ws + C.L.dla + (size_t)k * NI;
+        for (int r = 0; r < NI; ++r) { dsa[r] = T(0); dla[r] = T(0); }
+    }
+    for (int e = tid; e < NB * 9; e += NT) C.ws[C.L.nu + e] = T(0);
+    __syncthreads();
+    int status = CMPC_QP_MAX_ITER, it = 0;
+    T mu_hist = T(1e300);
+    for (it = 0; it < max_iter; ++it) {
+        Norms<T, ROBOT> nm{0, 0, 0, 0, 0, 0, 0, 0};
+        for (int k = tid; k < K1; k += NT) phase_residual<T, ROBOT>(C, k, nm);
+        T mx[6] = {nm.prim, nm.dual, nm.comp, nm.sp, nm.sd, nm.lmax};
+        block_reduce<T, NT, 6, 1>(mx, red);
+        T sm2[2] = {nm.mu, nm.cnt};
+        block_reduce<T, NT, 2, 0>(sm2, red);
+        const T prim = mx[0], dual = mx[1], comp = mx[2], sp = mx[3], sdd = mx[4], lmax = mx[5];
+        const T mu = sm2[0] / fmax(sm2[1], T(1));
+        if (!(prim == prim) || !(dual == dual) || !(mu == mu)) { status = CMPC_QP_NONFINITE; break; }
+        const T ep = eps_abs + eps_rel * sp, ed = eps_abs + eps_rel * sdd;
+        const T ec = eps_abs + eps_rel * fmax(T(1), lmax) * T(1e-3);
+        if (prim <= ep && dual <= ed && comp <= ec) { status = 1; break; }
+        mu_hist = mu;
+        // ---- factorization
+        for (int k = tid; k < K1; k += NT) phase_factor<T, ROBOT>(C, k);
+        __syncthreads();
+        for (int k = tid; k < K1; k += NT) phase_sblock<T, ROBOT>(C, k);
+        __syncthreads();
+        if (tid < 64) seq_factor(C.ws + C.L.Sd, C.ws + C.L.So, NB, sh);
+        __syncthreads();
+        // ---- predictor (affine) and corrector
+        T sigma_mu = T(0);
+        T alpha = T(1);
+        for (int corr = 0; corr < 2; ++corr) {
+            for (int k = tid; k < K1; k += NT) phase_w<T, ROBOT>(C, k, corr, sigma_mu);
+            __syncthreads();
+            for (int k = tid; k < K1; k += NT) phase_rhs<T, ROBOT>(C, k);
+            __syncthreads();
+            if (tid < 64) seq_solve(C.ws + C.L.Sd, C.ws + C.L.So, C.ws + C.L.rhs, C.ws + C.L.dnu, NB, sh);
+            __syncthreads();
+            T am[1] = {T(1)};
+            for (int k = tid; k < K1; k += NT) am[0] = fmin(am[0], phase_dz<T, ROBOT>(C, k, corr, sigma_mu));
+            block_reduce<T, NT, 1, 2>(am, red);
+            alpha = am[0];
+            if (corr == 0) {
+                T ma[1] = {T(0)};
+                for (int k = tid; k < K1; k += NT) ma[0] += mu_after<T, ROBOT>(C, k, alpha);
+                block_reduce<T, NT, 1, 0>(ma, red);
+                const T mu_aff = ma[0] / fmax(sm2[1], T(1));
+                const T sg = mu_aff / fmax(mu, T(1e-300));
+                sigma_mu = sg * sg * sg * mu;
+            }
+        }
+        alpha = fmin(T(1), eta * alpha);
+        for (int k = tid; k < K1; k += NT) phase_update<T, ROBOT>(C, k, alpha);
+        __syncthreads();
+    }
+    (void)mu_hist;
+    // ---- outputs: solution and multipliers
+    for (int k = tid; k < K1; k += NT) {
+        const T *x = C.var_x(k);
+        for (int i = 0; i < 9; ++i) d.xs[((size_t)b * K1 + k) * 9 + i] = x[i];
+        d.ts[(size_t)b * K1 + k] = C.ws[C.L.t + k];
+        if (k < N) { const T *u = C.var_u(k); for (int i = 0; i < NU; ++i) d.us[((size_t)b * N + k) * NU + i] = u[i]; }
+        const T *lm = C.ws + C.L.l + (size_t)k * NI;
+        for (int r = 0; r < NI; ++r) d.lams[((size_t)b * K1 + k) * NI + r] = C.present(k, r) ? lm[r] : T(0);
+    }
+    for (int e = tid; e < NB * 9; e += NT) d.nus[(size_t)b * NB * 9 + e] = C.ws[C.L.nu + e];
+    if (tid == 0) {
+        d.qp_status[b] = status;
+        d.qp_iters[b] = it;
+    }
+}
+
+#define INST(T, R) template __global__ void k_qp_ipm<T, R>(DevBuf<T>, int, int, T, T, T);
+INST(double, 0)
+INST(double, 1)
+INST(float, 0)
+INST(float, 1)
+#undef INST
+
+size_t ipm_workspace_elems(int N, int robot) {
+    return robot == 0 ? WsLayout(N, Rows<0>::NI, Robot<0>::NC).total : WsLayout(N, Rows<1>::NI, Robot<1>::NC).total;
+}
+
+}  // namespace cmpc

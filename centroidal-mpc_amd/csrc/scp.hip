@@ -1,0 +1,181 @@
+// SCP accept/reject step for every problem (one workgroup per problem).
+//
+// Replaces the body of solve_scp after the QP (reference src/scp_solver.py:149-177):
+//   * trust-region test ||X_sol - X_prev||_2 < radius with the SPECTRAL norm of the
+//     9 x (N+1) difference (quirk Q6): sigma_max^2 = lambda_max(D D'), D D' 9x9 Gram matrix,
+//     cyclic Jacobi eigenvalues (double);
+//   * model accuracy rho = sum_k ||nl_k[6:] - lin_k[6:]||^2 / sum_k ||lin_k||^2 over k < N
+//     (compute_model_accuracy :71-87, nonlinear rollout :243-255);
+//   * GuSTO updates: radius *= beta_fail | accept (+ radius = min(beta_succ r, r0)) |
+//     weight *= gamma_fail; QP failure ends the problem with status QP_FAILED (:146-148).
+// The linearization point is never updated, exactly as in the reference (quirk Q1).
+#include "common.hpp"
+
+namespace cmpc {
+
+enum { DEC_NONE = 0, DEC_ACCEPT = 1, DEC_REJECT_RHO = 2, DEC_REJECT_TR = 3, DEC_QP_FAILED = -1 };
+
+__device__ double jacobi_lambda_max(double (&a)[9][9]) {
+    for (int sweep = 0; sweep < 40; ++sweep) {
+        double off = 0.0, tot = 0.0;
+        for (int i = 0; i < 9; ++i)
+            for (int j = 0; j < 9; ++j) {
+                tot += a[i][j] * a[i][j];
+                if (i != j) off += a[i][j] * a[i][j];
+            }
+        if (off <= 1e-30 * tot || off == 0.0) break;
+        for (int p = 0; p < 8; ++p)
+            for (int q = p + 1; q < 9; ++q) {
+                const double apq = a[p][q];
+                if (apq == 0.0) continue;
+                const double theta = (a[q][q] - a[p][p]) / (2.0 * apq);
+                const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+                for (int k = 0; k < 9; ++k) {
+                    const double akp = a[k][p], akq = a[k][q];
+                    a[k][p] = c * akp - s * akq;
+                    a[k][q] = s * akp + c * akq;
+                }
+                for (int k = 0; k < 9; ++k) {
+                    const double apk = a[p][k], aqk = a[q][k];
+                    a[p][k] = c * apk - s * aqk;
+                    a[q][k] = s * apk + c * aqk;
+                }
+            }
+    }
+    double m = a[0][0];
+    for (int i = 1; i < 9; ++i) m = fmax(m, a[i][i]);
+    return m;
+}
+
+// x+ = x + dt F(x, u) for the knot-k contact data (integrate_model_one_step)
+template <typename T, int ROBOT>
+__device__ void step_dyn(const DevParams<T> &prm, const T *x, const T *u, const T *p, const T *R, const uint8_t *lg,
+                         T *o) {
+    constexpr int NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
+    const T m = prm.mass;
+    T F[9] = {(T(1) / m) * x[3], (T(1) / m) * x[4], (T(1) / m) * x[5], 0, 0, m * prm.gravity, 0, 0, 0};
+    for (int c = 0; c < NC; ++c) {
+        const T a = T(lg[c]);
+        const T *f = u + NUPC * c + FO;
+        T pc[3] = {p[3 * c] - x[0], p[3 * c + 1] - x[1], p[3 * c + 2] - x[2]};
+        T v[3];
+        cross3(pc, f, v);
+        if (ROBOT == 1) {
+            const T *Rc = R + 9 * c;
+            const T *cp = u + NUPC * c;
+            T q[3], w[3];
+            for (int z = 0; z < 3; ++z) q[z] = Rc[z * 3] * cp[0] + Rc[z * 3 + 1] * cp[1];
+            cross3(q, f, w);
+            for (int z = 0; z < 3; ++z) v[z] += w[z] + Rc[z * 3 + 2] * cp[5];
+        }
+        for (int z = 0; z < 3; ++z) { F[3 + z] += a * f[z]; F[6 + z] += a * v[z]; }
+    }
+    for (int i = 0; i < 9; ++i) o[i] = x[i] + F[i] * prm.dt;
+}
+
+template <typename T, int ROBOT>
+__global__ void __launch_bounds__(256) k_accept(DevBuf<T> d, int fixed_iters) {
+    constexpr int NC = Robot<ROBOT>::NC;
+    const int b = blockIdx.x;
+    if (b >= d.B) return;
+    ScpState &sc = d.scp[b];
+    if (!sc.active) return;
+    __shared__ T red[2 * 4];
+    __shared__ double gram[81];
+    __shared__ int dec_sh;
+    const int tid = threadIdx.x, N = d.N, K1 = N + 1;
+    const DevParams<T> &prm = d.params[d.class_id[b]];
+    const T *Xs = d.xs + (size_t)b * K1 * 9, *Us = d.us + (size_t)b * N * NU;
+    const T *Xb = d.Xbar + (size_t)b * K1 * 9, *Ub = d.Ubar + (size_t)b * N * NU;
+    const int qst = d.qp_status[b];
+    // ---- rho (fp of the compute type)
+    T acc[2] = {T(0), T(0)};
+    for (int k = tid; k < N; k += 256) {
+        const size_t kn = (size_t)b * N + k;
+        T nl[9];
+        step_dyn<T, ROBOT>(prm, Xs + (size_t)k * 9, Us + (size_t)k * NU, d.pos + kn * 3 * NC, d.rot + kn * 9 * NC,
+                           d.logic + kn * NC, nl);
+        const T *A = d.A + kn * 81, *Bm = d.Bu + kn * 9 * NU, *f = d.f + kn * 9;
+        T dx[9], du[NU];
+        for (int i = 0; i < 9; ++i) dx[i] = Xs[(size_t)k * 9 + i] - Xb[(size_t)k * 9 + i];
+        for (int i = 0; i < NU; ++i) du[i] = Us[(size_t)k * NU + i] - Ub[(size_t)k * NU + i];
+        for (int i = 0; i < 9; ++i) {
+            T lin = f[i];
+            for (int j = 0; j < 9; ++j) lin = fma(A[i * 9 + j], dx[j], lin);
+            for (int j = 0; j < NU; ++j) lin = fma(Bm[i * NU + j], du[j], lin);
+            if (i >= 6) acc[0] += sq(nl[i] - lin);
+            acc[1] += lin * lin;
+        }
+    }
+    block_reduce<T, 256, 2, 0>(acc, red);
+    const double rho = double(acc[0]) / double(acc[1]);
+    // ---- Gram matrix of X_sol - Xbar (double)
+    if (tid < 81) {
+        const int i = tid / 9, j = tid % 9;
+        double g = 0.0;
+        for (int k = 0; k < K1; ++k)
+            g += (double(Xs[(size_t)k * 9 + i]) - double(Xb[(size_t)k * 9 + i])) *
+                 (double(Xs[(size_t)k * 9 + j]) - double(Xb[(size_t)k * 9 + j]));
+        gram[tid] = g;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        double a[9][9];
+        for (int e = 0; e < 81; ++e) a[e / 9][e % 9] = gram[e];
+        const double tr = sqrt(fmax(jacobi_lambda_max(a), 0.0));
+        int dec;
+        sc.qp_status = qst;
+        sc.qp_iters = d.qp_iters[b];
+        sc.tr_norm = tr;
+        sc.rho = rho;
+        if (qst != 1) {
+            dec = DEC_QP_FAILED;
+            sc.success = 0;
+        } else if (tr < sc.radius) {
+            if (rho > prm.rho1) {
+                sc.radius *= prm.beta_fail;
+                sc.success = 0;
+                dec = DEC_REJECT_RHO;
+            } else {
+                sc.success = 1;
+                sc.n_accepted += 1;
+                dec = DEC_ACCEPT;
+                if (rho < prm.rho0) sc.radius = fmin(prm.beta_succ * sc.radius, prm.tr_radius0);
+            }
+        } else {
+            sc.weight *= prm.gamma_fail;
+            sc.success = 0;
+            dec = DEC_REJECT_TR;
+        }
+        sc.decision = dec;
+        sc.iter += 1;
+        if (dec == DEC_QP_FAILED) {
+            sc.status = CMPC_SCP_QP_FAILED;
+            if (!fixed_iters) sc.active = 0;
+        } else if (!fixed_iters) {
+            const bool cont = sc.iter < prm.max_iterations && sc.weight < prm.omega_max && !(sc.iter != 0 && sc.success);
+            if (!cont) {
+                sc.active = 0;
+                sc.status = sc.success ? CMPC_SCP_CONVERGED : CMPC_SCP_MAX_ITER;
+            }
+        } else if (sc.status == CMPC_SCP_RUNNING && sc.success) {
+            sc.status = CMPC_SCP_CONVERGED;
+        }
+        dec_sh = dec;
+    }
+    __syncthreads();
+    if (dec_sh != DEC_ACCEPT) return;
+    // accepted: keep X, U and this iteration's LQR gains / covariances
+    for (int e = tid; e < K1 * 9; e += 256) d.Xacc[(size_t)b * K1 * 9 + e] = Xs[e];
+    for (int e = tid; e < N * NU; e += 256) d.Uacc[(size_t)b * N * NU + e] = Us[e];
+    for (int e = tid; e < N * NU * 9; e += 256) d.Kacc[(size_t)b * N * NU * 9 + e] = d.K[(size_t)b * N * NU * 9 + e];
+    for (int e = tid; e < K1 * 81; e += 256) d.Sacc[(size_t)b * K1 * 81 + e] = d.Sig[(size_t)b * K1 * 81 + e];
+}
+
+template __global__ void k_accept<double, 0>(DevBuf<double>, int);
+template __global__ void k_accept<double, 1>(DevBuf<double>, int);
+template __global__ void k_accept<float, 0>(DevBuf<float>, int);
+template __global__ void k_accept<float, 1>(DevBuf<float>, int);
+
+}  // namespace cmpc

@@ -1,0 +1,138 @@
+/*
+ * cmpc.h -- C ABI of the MI355X batched SCP centroidal-MPC solver (libcmpc.so).
+ *
+ * Drop-in boundary for the reference's per-SCP-iteration hot path
+ * (ahmadgazar/centroidal-MPC, paths relative to the reference root):
+ *
+ *   reference interface                                    replaced by
+ *   -----------------------------------------------------  --------------------------------
+ *   Centroidal_model.__init__ contact / warm-start arrays   cmpc_upload
+ *     src/centroidal_model.py:127-187
+ *   Centroidal_model.compute_trajectory_data (JAX, fp32)    cmpc_linearize / cmpc_get_linearization
+ *     src/centroidal_model.py:189-291
+ *   sum_up_all_costs / stack_up_all_constraints (numpy)     cmpc_assemble / cmpc_export_qp
+ *     src/scp_solver.py:10-48, src/cost.py, src/constraints.py
+ *   solve_subproblem: osqp.OSQP().setup(P,q,A,l,u,...)      cmpc_qp_solve / cmpc_get_qp_solution
+ *     .solve()   src/scp_solver.py:59-68
+ *   compute_model_accuracy / trust-region test / accept     cmpc_scp_iterate (one full iteration)
+ *     src/scp_solver.py:71-87,151-177
+ *   solve_scp (while loop)                                  cmpc_solve_scp / cmpc_get_solution
+ *     src/scp_solver.py:118-179
+ *
+ * Conventions: every function returns 0 on success and a negative code on error
+ * (cmpc_last_error(h) gives the message; no C++ exception crosses the ABI).  Host
+ * buffers are C-contiguous float64 (int8/int32 where stated) and owned by the caller;
+ * the library copies in/out.  Device state is owned by the handle.  A handle is bound to
+ * one device and is not thread-safe.  Calls that launch GPU work are asynchronous on the
+ * handle's stream unless documented as synchronous; getters synchronize.
+ *
+ * Layouts (B problems, horizon N, nc contacts, nu = 12 controls):
+ *   logic (B,N,nc) int8 | pos (B,N,nc,3) | rot (B,N,nc,3,3) | Xbar (B,N+1,9) | Ubar (B,N,nu)
+ *   f (B,N,9) | A (B,N,9,9) | Bu (B,N,9,nu) | C (B,N,9,3nc) | K (B,N,nu,9) | Sigma (B,N+1,9,9)
+ */
+#ifndef CMPC_H
+#define CMPC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CMPC_ROBOT_SOLO12 0
+#define CMPC_ROBOT_TALOS 1
+#define CMPC_PREC_F64 0
+#define CMPC_PREC_F32 1
+
+/* per-problem SCP / QP status codes (OSQP-compatible values) */
+#define CMPC_QP_SOLVED 1
+#define CMPC_QP_MAX_ITER (-2)
+#define CMPC_QP_PRIMAL_INFEASIBLE (-3)
+#define CMPC_QP_NONFINITE (-10)
+
+#define CMPC_SCP_RUNNING 0
+#define CMPC_SCP_CONVERGED 1      /* loop ended after an accepted iteration */
+#define CMPC_SCP_MAX_ITER 2       /* loop ended on max_iterations / omega_max */
+#define CMPC_SCP_QP_FAILED (-1)   /* reference returns False (src/scp_solver.py:146-148) */
+
+typedef struct cmpc_handle_s *cmpc_handle;
+
+/* Parameters of one problem class: the conf_* attributes the hot path reads
+ * (config/conf_solo12_trot.py:7-94).  Matrices are row-major; R and cov_w use the
+ * top-left nu x nu / 3nc x 3nc corner. */
+typedef struct {
+    double mass, gravity, dt, mu, beta_u;
+    double foot_range[4];   /* lxp, lxn, lyp, lyn (TALOS CoP box) */
+    double Wx[9];           /* diag(state_cost_weights) */
+    double Wu[12];          /* diag(control_cost_weights) */
+    double Q[81];           /* LQR state weight */
+    double R[144];          /* LQR control weight */
+    double cov_w[144];      /* contact-position noise (3nc x 3nc) */
+    double cov_eta[81];     /* additive noise (already scaled by dt) */
+    int32_t stochastic;     /* STOCHASTIC_OCP: chance-constraint back-off in friction rows */
+    int32_t tracking;       /* solo12 && !DYNAMICS_FIRST: state tracking cost */
+    /* scp_params */
+    double tr_radius0, omega0, omega_max, rho0, rho1, beta_succ, beta_fail, gamma_fail;
+    double convergence_threshold;
+    int32_t max_iterations;
+} cmpc_params;
+
+/* QP solver settings (defaults by cmpc_default_qp_settings) */
+typedef struct {
+    int32_t max_iter;       /* interior-point iterations (default 60) */
+    double eps_abs;         /* absolute tolerance (fp64 default 1e-9) */
+    double eps_rel;         /* relative tolerance (fp64 default 1e-9) */
+    double step_fraction;   /* fraction-to-boundary (default 0.99) */
+} cmpc_qp_settings;
+
+/* Per-phase device timings of the last cmpc_scp_iterate (milliseconds, HIP events). */
+typedef struct {
+    float linearize_ms, assemble_ms, qp_ms, accept_ms, total_ms;
+} cmpc_timing;
+
+int cmpc_create(cmpc_handle *out, int device, int robot, int N, int max_batch, int precision);
+int cmpc_destroy(cmpc_handle h);
+const char *cmpc_last_error(cmpc_handle h);
+int cmpc_version(void);
+
+int cmpc_default_qp_settings(int precision, cmpc_qp_settings *s);
+int cmpc_set_qp_settings(cmpc_handle h, const cmpc_qp_settings *s);
+int cmpc_set_params(cmpc_handle h, int n_classes, const cmpc_params *classes);
+
+/* Copy B problems to the device and reset their SCP state
+ * (weight = omega0, radius = trust_region_radius0, iteration 0). */
+int cmpc_upload(cmpc_handle h, int B, const int32_t *class_id, const int8_t *logic, const double *pos,
+                const double *rot, const double *Xbar, const double *Ubar);
+
+/* ---- hot-path phases (asynchronous) ---- */
+int cmpc_linearize(cmpc_handle h);                 /* f, A, Bu, C, K, Sigma for all problems */
+int cmpc_assemble(cmpc_handle h);                  /* structured QP from linearization + SCP state */
+int cmpc_qp_solve(cmpc_handle h);                  /* batched interior-point QP */
+int cmpc_accept(cmpc_handle h, int fixed_iters);   /* trust-region test, rho, accept/reject */
+/* One full SCP iteration for every active problem: linearize -> assemble -> QP -> accept.
+ * fixed_iters != 0: every problem iterates (benchmark fixed-K mode); 0: finished problems
+ * are skipped (reference semantics). */
+int cmpc_scp_iterate(cmpc_handle h, int fixed_iters);
+/* Run the reference's while loop to completion (synchronous). */
+int cmpc_solve_scp(cmpc_handle h, int fixed_iters, int *n_iterations_out);
+int cmpc_synchronize(cmpc_handle h);
+
+/* ---- getters (synchronous; NULL pointers are skipped) ---- */
+int cmpc_get_linearization(cmpc_handle h, double *f, double *A, double *Bu, double *C, double *K,
+                           double *Sigma);
+int cmpc_qp_sizes(cmpc_handle h, int32_t *n, int32_t *m, int32_t *nnzP, int32_t *nnzA);
+/* CSC export of problem b's QP in the reference's exact row order (parity/debug only). */
+int cmpc_export_qp(cmpc_handle h, int b, double *P_x, int32_t *P_i, int32_t *P_p, double *q, double *A_x,
+                   int32_t *A_i, int32_t *A_p, double *l, double *u);
+/* z in the reference's variable layout (B, n) and y in its row layout (B, m). */
+int cmpc_get_qp_solution(cmpc_handle h, double *z, double *y, int32_t *status, int32_t *iters);
+int cmpc_get_solution(cmpc_handle h, double *X, double *U, double *K, double *Sigma, int32_t *n_accepted,
+                      int32_t *iterations, int32_t *scp_status, double *weight, double *radius);
+int cmpc_get_iteration_log(cmpc_handle h, double *tr_norm, double *rho, int32_t *qp_status,
+                           int32_t *qp_iters, int32_t *decision);
+int cmpc_get_timing(cmpc_handle h, cmpc_timing *t);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CMPC_H */

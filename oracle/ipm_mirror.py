@@ -1,0 +1,275 @@
+"""CPU mirror of the GPU structured interior-point QP (same algorithm, numpy).  TEST INFRASTRUCTURE.
+
+This is NOT a restatement of the reference; it mirrors the algorithm of the GPU kernel
+(centroidal-mpc_amd/csrc/qp_ipm.hip) step by step so that a GPU mismatch can be localized
+to one phase.  Parity of the GPU answer itself is checked against ``osqp_admm`` (the
+reference's algorithm) and the solver-independent ``kkt`` residuals.
+
+Structured QP per problem (all blocks per knot k):
+  min  sum_k 1/2 x_k'Wx x_k + qx_k'x_k + t_k + sum_{k<N} 1/2 u_k'Wu u_k
+  s.t. x_0 = xbar_0;  A_k x_k + B_k u_k - x_{k+1} = r_k (k<N);  x_N = xbar_N
+       TR:   s_j'L_k + cw t_k <= btr_kj  (j<8),  -t_k <= 0          (L = x[6:9], cw = -1/omega)
+       fric: G_kij' f_ki <= h_kij (active contacts, j<4)
+       CoP:  lo <= cop_kid <= hi (TALOS, active contacts)
+Mehrotra predictor-corrector.  The Newton system is reduced to the dual Schur complement
+S = E Phi^-1 E' (Phi = H + G'DG is block diagonal per knot; t is eliminated in each knot),
+which is block tridiagonal with N+2 blocks of 9x9 and is factorized by block Cholesky.
+"""
+import numpy as np
+
+PENUM = np.array([[(-1) ** (j // (2 ** i)) for i in range(3)] for j in range(8)], float)
+
+
+class StructQP:
+    """Structured subproblem (built by ``from_arrays``)."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+    @staticmethod
+    def from_arrays(N, robot, nc, Wx, Wu, Xbar, Ubar, A, Bm, f, logic, rot, mu, weight, radius,
+                    tracking=True, fric_h=None, foot_range=(0.01, 0.01, 0.01, 0.01)):
+        """Xbar (N+1,9), Ubar (N,nu), A (N,9,9), Bm (N,9,nu), f (N,9), logic (N,nc), rot (N,nc,3,3)."""
+        nu = Ubar.shape[1]
+        r = np.einsum('kij,kj->ki', A, Xbar[:N]) + np.einsum('kij,kj->ki', Bm, Ubar) - f
+        ml = mu / np.sqrt(2)
+        Fmu = np.array([[1., 0., -ml], [-1., 0., -ml], [0., 1., -ml], [0., -1., -ml]])
+        G = np.einsum('rj,kimj->kirm', Fmu, rot)          # F_mu R^T  -> (N, nc, 4, 3)
+        if fric_h is None:
+            fric_h = np.zeros((N, nc, 4))
+        qx = -(Wx[None, :] * Xbar) if tracking else np.zeros_like(Xbar)
+        btr = radius + Xbar[:, 6:9] @ PENUM.T               # (N+1, 8)
+        return StructQP(N=N, robot=robot, nc=nc, nu=nu, nupc=nu // nc, Wx=np.asarray(Wx, float),
+                        Wu=np.asarray(Wu, float), qx=qx, A=A, Bm=Bm, r=r, x0=Xbar[0].copy(),
+                        xN=Xbar[N].copy(), btr=btr, cw=-1.0 / weight, G=G, fh=fric_h,
+                        fmask=logic.astype(bool), foot_range=foot_range, Xbar=Xbar, Ubar=Ubar)
+
+
+def _fslot(qp):
+    return 0 if qp.robot == 'solo12' else 2
+
+
+def solve(qp, eps=1e-9, max_iter=60, eta=0.99, verbose=False):
+    N, nc, nu, nupc = qp.N, qp.nc, qp.nu, qp.nupc
+    fo = _fslot(qp)
+    talos = qp.robot != 'solo12'
+    # ---- variables ----
+    x = qp.Xbar.copy(); u = qp.Ubar.copy(); t = np.zeros(N + 1); nu_ = np.zeros((N + 2, 9))
+    fm = qp.fmask[:, :, None].astype(float) * np.ones((1, 1, 4))        # (N, nc, 4)
+    cm = qp.fmask[:, :, None, None].astype(float) * np.ones((1, 1, 2, 2)) if talos else None
+    lxp, lxn, lyp, lyn = qp.foot_range
+    cop_hi = np.array([lxp, lyp]); cop_lo = np.array([-lxn, -lyn])
+
+    def ineq_val(x, u, t):
+        """g'z - h for every inequality (so feasibility is <= 0)."""
+        L = x[:, 6:9]
+        v_tr = L @ PENUM.T + qp.cw * t[:, None] - qp.btr
+        v_sl = -t
+        f = u.reshape(N, nc, nupc)[:, :, fo:fo + 3]
+        v_fr = np.einsum('kirm,kim->kir', qp.G, f) - qp.fh
+        out = [v_tr, v_sl, v_fr]
+        if talos:
+            cop = u.reshape(N, nc, nupc)[:, :, 0:2]
+            v_cp = np.stack([cop - cop_hi, -cop + cop_lo], axis=3)         # (N, nc, 2dim, 2side)
+            out.append(v_cp)
+        return out
+
+    masks = [np.ones((N + 1, 8)), np.ones(N + 1), fm] + ([cm] if talos else [])
+    vals = ineq_val(x, u, t)
+    s = [np.where(mk > 0, np.maximum(-v, 1.0), 1.0) for v, mk in zip(vals, masks)]
+    lam = [mk * 1.0 for mk in masks]
+    m_tot = sum(mk.sum() for mk in masks)
+
+    def GT(lams):
+        """G' lambda split into (x (N+1,9), t (N+1,), u (N,nu))."""
+        gx = np.zeros((N + 1, 9)); gt = np.zeros(N + 1); gu = np.zeros((N, nc, nupc))
+        gx[:, 6:9] = lams[0] @ PENUM
+        gt += qp.cw * lams[0].sum(axis=1) - lams[1]
+        gu[:, :, fo:fo + 3] = np.einsum('kirm,kir->kim', qp.G, lams[2])
+        if talos:
+            gu[:, :, 0:2] += lams[3][..., 0] - lams[3][..., 1]
+        return gx, gt, gu.reshape(N, nu)
+
+    def Gz(dx, du, dt_):
+        L = dx[:, 6:9]
+        out = [L @ PENUM.T + qp.cw * dt_[:, None], -dt_,
+               np.einsum('kirm,kim->kir', qp.G, du.reshape(N, nc, nupc)[:, :, fo:fo + 3])]
+        if talos:
+            cop = du.reshape(N, nc, nupc)[:, :, 0:2]
+            out.append(np.stack([cop, -cop], axis=3))
+        return out
+
+    def ET(nv):
+        ex = np.zeros((N + 1, 9)); eu = np.zeros((N, nu))
+        ex[0] += nv[0]
+        ex[:N] += np.einsum('kji,kj->ki', qp.A, nv[1:N + 1])
+        ex[1:N + 1] -= nv[1:N + 1]
+        ex[N] += nv[N + 1]
+        eu += np.einsum('kji,kj->ki', qp.Bm, nv[1:N + 1])
+        return ex, eu
+
+    def Ez(x, u):
+        e = np.zeros((N + 2, 9))
+        e[0] = x[0]
+        e[1:N + 1] = np.einsum('kij,kj->ki', qp.A, x[:N]) + np.einsum('kij,kj->ki', qp.Bm, u) - x[1:]
+        e[N + 1] = x[N]
+        return e
+
+    e_rhs = np.zeros((N + 2, 9)); e_rhs[0] = qp.x0; e_rhs[1:N + 1] = qp.r; e_rhs[N + 1] = qp.xN
+    it = 0; status = -2
+    hist = []
+    for it in range(1, max_iter + 1):
+        # ---- residuals ----
+        gx, gt, gu = GT(lam)
+        ex, eu = ET(nu_)
+        rdx = qp.Wx * x + qp.qx + ex + gx
+        rdt = 1.0 + gt
+        rdu = qp.Wu * u + eu + gu
+        rde = Ez(x, u) - e_rhs
+        vals = ineq_val(x, u, t)
+        rdi = [(v + si) * mk for v, si, mk in zip(vals, s, masks)]
+        mu_ = sum((si * li * mk).sum() for si, li, mk in zip(s, lam, masks)) / m_tot
+        # ---- termination (OSQP-style relative criteria on the reference problem) ----
+        prim = max(np.abs(rde).max(), max(np.maximum(v * mk, 0).max() for v, mk in zip(vals, masks)))
+        dual = max(np.abs(rdx).max(), np.abs(rdt).max(), np.abs(rdu).max())
+        comp = max((si * li * mk).max() for si, li, mk in zip(s, lam, masks))
+        scale_p = max(np.abs(Ez(x, u)).max(), np.abs(e_rhs).max(), 1.0)
+        scale_d = max(np.abs(qp.Wx * x).max(), np.abs(qp.Wu * u).max(), np.abs(qp.qx).max(), 1.0)
+        hist.append((it, prim, dual, comp, mu_))
+        if verbose:
+            print('it %2d prim %.2e dual %.2e comp %.2e mu %.2e' % (it, prim, dual, comp, mu_))
+        if prim <= eps * scale_p and dual <= eps * scale_d and comp <= eps * scale_d:
+            status = 1
+            break
+        # ---- factorization ----
+        D = [li / si * mk for li, si, mk in zip(lam, s, masks)]
+        # x/t block: Phi_LL, Phi_Lt, Phi_tt
+        PhiLL = np.zeros((N + 1, 3, 3)) + np.diag(qp.Wx[6:9])[None]
+        PhiLL += np.einsum('kj,ja,jb->kab', D[0], PENUM, PENUM)
+        PhiLt = qp.cw * (D[0] @ PENUM)
+        Phitt = qp.cw ** 2 * D[0].sum(axis=1) + D[1]
+        MLLinv = PhiLL - np.einsum('ka,kb->kab', PhiLt, PhiLt) / Phitt[:, None, None]
+        ML = np.linalg.inv(MLLinv)                       # (N+1,3,3)
+        Mfull = np.zeros((N + 1, 9, 9))
+        Mfull[:, np.arange(6), np.arange(6)] = 1.0 / qp.Wx[:6]
+        Mfull[:, 6:9, 6:9] = ML
+        # u blocks, computed stably (D can reach 1e15+): with K = D^-1 + G W^-1 G' (4x4 SPD),
+        # Phi_u^-1 = W^-1 - W^-1 G' K^-1 G W^-1 and Phi_u^-1 G' D = W^-1 G' K^-1 (push-through).
+        Wu_b = qp.Wu.reshape(nc, nupc)
+        Winv = np.zeros((N, nc, nupc, nupc)) + np.stack([np.diag(1.0 / Wu_b[i]) for i in range(nc)])[None]
+        if talos:
+            # CoP rows are bound rows on single coordinates: fold them into the diagonal
+            # (D <= 1/lo-side slack, bounded by the box width, so no cancellation)
+            dcop = D[3].sum(axis=3)                                   # (N, nc, 2)
+            for d in range(2):
+                Winv[:, :, d, d] = 1.0 / (Wu_b[None, :, d] + dcop[:, :, d])
+        Gw = np.einsum('kirm,kimn->kirn', qp.G, Winv[:, :, fo:fo + 3, fo:fo + 3])    # G W^-1 (N,nc,4,3)
+        Dinv_f = np.where(fm > 0, s[2] / np.where(fm > 0, lam[2], 1.0), 1.0)
+        Kf = np.einsum('kirn,kiqn->kirq', Gw, qp.G) + Dinv_f[..., None] * np.eye(4)
+        Kf = np.where(fm[..., None] > 0, Kf, np.eye(4))                 # inactive contacts: identity
+        Gw = Gw * fm[..., None]
+        Kf_inv = np.linalg.inv(Kf)
+        Phiuinv = Winv.copy()
+        Phiuinv[:, :, fo:fo + 3, fo:fo + 3] -= np.einsum('kirn,kirq,kiqm->kinm', Gw, Kf_inv, Gw)
+        # S blocks
+        Sd = np.zeros((N + 2, 9, 9)); So = np.zeros((N + 1, 9, 9))
+        Sd[0] = Mfull[0]
+        Bblk = qp.Bm.reshape(N, 9, nc, nupc)
+        BPB = np.einsum('kaic,kicd,kbid->kab', Bblk, Phiuinv, Bblk)
+        Sd[1:N + 1] = np.einsum('kai,kij,kbj->kab', qp.A, Mfull[:N], qp.A) + BPB + Mfull[1:]
+        Sd[N + 1] = Mfull[N]
+        So[0] = Mfull[0] @ qp.A[0].T
+        So[1:N] = -np.einsum('kij,kbj->kib', Mfull[1:N], qp.A[1:N])
+        So[N] = -Mfull[N]
+        # block Cholesky: Lc[j] lower, Lo[j] = S_{j+1,j} Lc[j]^-T
+        Lc = np.zeros_like(Sd); Lo = np.zeros_like(So)
+        Sh = Sd[0].copy()
+        for j in range(N + 2):
+            Lc[j] = np.linalg.cholesky(Sh)
+            if j < N + 1:
+                Lo[j] = np.linalg.solve(Lc[j], So[j]).T        # (S_{j,j+1})^T Lc^-T
+                Sh = Sd[j + 1] - Lo[j] @ Lo[j].T
+
+        def phi_solve(vx, vt, vu):
+            """Phi^-1 (vx, vt, vu) with t eliminated per knot."""
+            vx = vx.copy()
+            vx[:, 6:9] -= PhiLt * (vt / Phitt)[:, None]
+            dx = np.einsum('kij,kj->ki', Mfull, vx)
+            dt_ = (vt - np.einsum('ka,ka->k', PhiLt, dx[:, 6:9])) / Phitt
+            du = np.einsum('kiab,kib->kia', Phiuinv, vu.reshape(N, nc, nupc)).reshape(N, nu)
+            return dx, dt_, du
+
+        def newton(rc):
+            # rhat_i = r_i - r_c / lambda ; x/t rows use the Phi form, friction rows the stable form
+            rhat = [(ri - c / np.where(mk > 0, li, 1.0)) * mk for ri, c, li, mk in zip(rdi, rc, lam, masks)]
+            w = [d * rh for d, rh in zip(D, rhat)]
+            w[2] = np.zeros_like(w[2])
+            gx_, gt_, gu_ = GT(w)
+            vx, vt, vu = rdx + gx_, rdt + gt_, rdu + gu_
+            wx, wt, wu = phi_solve(vx, vt, vu)
+            # friction particular part: W^-1 G' K^-1 rhat_fric
+            kr = np.einsum('kirq,kiq->kir', Kf_inv, rhat[2])
+            wu_f = np.zeros((N, nc, nupc))
+            wu_f[:, :, fo:fo + 3] = np.einsum('kirn,kir->kin', Gw, kr)
+            wu = wu + wu_f.reshape(N, nu)
+            rhs = rde - Ez(wx, wu)
+            # forward / backward block substitution
+            y = np.zeros((N + 2, 9))
+            for j in range(N + 2):
+                b = rhs[j] - (Lo[j - 1] @ y[j - 1] if j > 0 else 0)
+                y[j] = np.linalg.solve(Lc[j], b)
+            dnu = np.zeros((N + 2, 9))
+            for j in range(N + 1, -1, -1):
+                b = y[j] - (Lo[j].T @ dnu[j + 1] if j < N + 1 else 0)
+                dnu[j] = np.linalg.solve(Lc[j].T, b)
+            ex_, eu_ = ET(dnu)
+            ax, at, au = phi_solve(ex_, np.zeros(N + 1), eu_)
+            dx = -wx - ax; dt_ = -wt - at; du = -wu - au
+            gz = Gz(dx, du, dt_)
+            dl = [(d * (g + rh)) * mk for d, g, rh, mk in zip(D, gz, rhat, masks)]
+            # friction: dlam = K^-1 (G W^-1 v + rhat), v = -(r_d,u + (E'dnu)_u)  (no D * r products)
+            vfull = -(rdu + eu_)
+            if talos:
+                vtmp = vfull.reshape(N, nc, nupc).copy()
+            vf = vfull.reshape(N, nc, nupc)[:, :, fo:fo + 3]
+            dl[2] = np.einsum('kirq,kiq->kir', Kf_inv, np.einsum('kirn,kin->kir', Gw, vf) + rhat[2]) * fm
+            ds = [(-ri - g) * mk for ri, g, mk in zip(rdi, gz, masks)]
+            return dx, dt_, du, dnu, dl, ds
+
+        def max_step(v, dv, mk):
+            neg = (dv < 0) & (mk > 0)
+            if not np.any(neg):
+                return 1.0
+            return min(1.0, float(np.min(-v[neg] / dv[neg])))
+
+        rc_aff = [si * li * mk for si, li, mk in zip(s, lam, masks)]
+        dx, dt_, du, dnu, dl, ds = newton(rc_aff)
+        a_aff = min(min(max_step(si, dsi, mk) for si, dsi, mk in zip(s, ds, masks)),
+                    min(max_step(li, dli, mk) for li, dli, mk in zip(lam, dl, masks)))
+        mu_aff = sum(((si + a_aff * dsi) * (li + a_aff * dli) * mk).sum()
+                     for si, dsi, li, dli, mk in zip(s, ds, lam, dl, masks)) / m_tot
+        sigma = (mu_aff / mu_) ** 3
+        rc = [(si * li + dsi * dli - sigma * mu_) * mk for si, li, dsi, dli, mk in zip(s, lam, ds, dl, masks)]
+        dx, dt_, du, dnu, dl, ds = newton(rc)
+        a = min(min(max_step(si, dsi, mk) for si, dsi, mk in zip(s, ds, masks)),
+                min(max_step(li, dli, mk) for li, dli, mk in zip(lam, dl, masks)))
+        a = min(1.0, eta * a)
+        x = x + a * dx; t = t + a * dt_; u = u + a * du; nu_ = nu_ + a * dnu
+        s = [np.where(mk > 0, si + a * dsi, 1.0) for si, dsi, mk in zip(s, ds, masks)]
+        lam = [(li + a * dli) * mk for li, dli, mk in zip(lam, dl, masks)]
+    return dict(x=x, u=u, t=t, nu=nu_, lam=lam, s=s, status=status, iters=it, hist=hist)
+
+
+def to_z(qp, sol):
+    """Pack into the reference's z layout [x | u | t | s(=0)]."""
+    N = qp.N
+    return np.concatenate([sol['x'].ravel(), sol['u'].ravel(), sol['t'], np.zeros(N)])
+
+
+def to_y(qp, sol):
+    """Multipliers in the reference's row layout (init | dyn | final | friction | TR | slack), solo12."""
+    N, nc = qp.N, qp.nc
+    fr = np.zeros((nc, N, 5))
+    fr[:, :, :4] = np.transpose(sol['lam'][2], (1, 0, 2))
+    return np.concatenate([sol['nu'][0], sol['nu'][1:N + 1].ravel(), sol['nu'][N + 1], fr.ravel(),
+                           sol['lam'][0].ravel(), sol['lam'][1]])
