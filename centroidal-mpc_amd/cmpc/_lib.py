@@ -49,7 +49,8 @@ EXPORTS = ['cmpc_create', 'cmpc_destroy', 'cmpc_last_error', 'cmpc_version', 'cm
            'cmpc_set_qp_settings', 'cmpc_set_params', 'cmpc_upload', 'cmpc_linearize', 'cmpc_assemble',
            'cmpc_qp_solve', 'cmpc_accept', 'cmpc_scp_iterate', 'cmpc_solve_scp', 'cmpc_synchronize',
            'cmpc_get_linearization', 'cmpc_qp_sizes', 'cmpc_export_qp', 'cmpc_get_qp_solution',
-           'cmpc_get_solution', 'cmpc_get_iteration_log', 'cmpc_get_timing']
+           'cmpc_get_solution', 'cmpc_get_iteration_log', 'cmpc_get_timing', 'cmpc_timing_begin',
+           'cmpc_timing_end', 'cmpc_get_qp_iterations_total']
 
 _lib = None
 
@@ -90,6 +91,9 @@ def load():
         'cmpc_get_solution': (i32, [h, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
         'cmpc_get_iteration_log': (i32, [h, vp, vp, vp, vp, vp]),
         'cmpc_get_timing': (i32, [h, P(Timing)]),
+        'cmpc_timing_begin': (i32, [h]),
+        'cmpc_timing_end': (i32, [h, P(Timing), P(ctypes.c_int)]),
+        'cmpc_get_qp_iterations_total': (i32, [h, P(ctypes.c_int64)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -273,3 +277,17 @@ class Solver:
         self._chk(self.lib.cmpc_get_timing(self.h, ctypes.byref(t)), 'cmpc_get_timing')
         return dict(linearize_ms=t.linearize_ms, assemble_ms=t.assemble_ms, qp_ms=t.qp_ms,
                     accept_ms=t.accept_ms, total_ms=t.total_ms)
+
+    def timing_begin(self):
+        self._chk(self.lib.cmpc_timing_begin(self.h), 'cmpc_timing_begin')
+
+    def timing_end(self):
+        t = Timing(); n = ctypes.c_int(0)
+        self._chk(self.lib.cmpc_timing_end(self.h, ctypes.byref(t), ctypes.byref(n)), 'cmpc_timing_end')
+        return dict(linearize_ms=t.linearize_ms, assemble_ms=t.assemble_ms, qp_ms=t.qp_ms,
+                    accept_ms=t.accept_ms, total_ms=t.total_ms, iterations=n.value)
+
+    def qp_iterations_total(self):
+        v = ctypes.c_int64(0)
+        self._chk(self.lib.cmpc_get_qp_iterations_total(self.h, ctypes.byref(v)), 'cmpc_get_qp_iterations_total')
+        return int(v.value)

@@ -8,10 +8,10 @@ here, so problems are synthesized:
   gait dict; nbSteps is raised until the plan covers N knots, then the plan is truncated to
   N (what the reference does when conf.N < plan length); per-problem foot xy jitter
   U(-0.01, 0.01) m and, for trot/bound, stepLength ~ U(0.08, 0.16);
-* warm start (N+1, 9): CoM xy follows the centroid of the stance feet (smoothed), CoM z
-  = nominal height + N(0, 0.003^2), linear momentum = m * finite-difference velocity,
-  angular momentum smoothed N(0, 0.01^2)
-  (all noise terms are 9-tap moving averages, so the warm start is smooth);
+* warm start (N+1, 9): a rollout of the centroidal dynamics (src/centroidal_model.py:189-212)
+  whose contact forces track the smoothed stance-foot centroid and the nominal CoM height
+  inside the friction pyramid (so the SCP subproblem is feasible, as with a DDP warm start),
+  plus smooth noise under a sin^2(pi k / N) envelope that vanishes at both ends;
 * Ubar: the reference rule [1e-3, 1e-3, m*9.81/#active] at rows 3i..3i+2 of every active
   contact (src/centroidal_model.py:176-183; also for TALOS, quirk Q11).
 Seed: numpy default_rng(1000 * cfg_seed + b).
@@ -56,30 +56,56 @@ def contact_plan(conf, N, rng=None, jitter=True):
     return contact_arrays(traj, N)
 
 
-def warm_start(conf, logic, pos, rng, mass, com_z):
-    """Synthetic DDP-like centroidal warm start, (N+1, 9)."""
+def warm_start(conf, logic, pos, rng, mass, com_z, gravity=-9.81, robot='solo12'):
+    """Synthetic DDP-like centroidal warm start, (N+1, 9).
+
+    A whole-body DDP warm start is dynamically consistent; a synthetic one must be too, or the
+    SCP subproblem is infeasible (a random final state is unreachable under the friction
+    pyramid).  So the states are a rollout of the centroidal dynamics driven by contact
+    forces that track the smoothed stance-foot centroid (PD on the CoM, forces kept strictly
+    inside the friction pyramid), plus smooth noise that vanishes at both ends."""
     N, nc = logic.shape
-    cxy = np.zeros((N + 1, 2))
+    dt = conf.dt
+    nupc = 3 if robot == 'solo12' else 6
+    fo = 0 if robot == 'solo12' else 2
+    cd = np.zeros((N + 2, 2))
     for k in range(N):
-        act = logic[k] > 0
-        cxy[k] = pos[k, act, :2].mean(axis=0)
-    cxy[N] = cxy[N - 1]
-    # moving-average smoothing, edge-padded
-    w = 9
-    pad = np.pad(cxy, ((w // 2, w // 2), (0, 0)), mode='edge')
-    ker = np.ones(w) / w
-    cxy = np.stack([np.convolve(pad[:, i], ker, mode='valid') for i in range(2)], axis=1)
+        cd[k] = pos[k, logic[k] > 0, :2].mean(axis=0)
+    cd[N:] = cd[N - 1]
+    w = 15
+    pad = np.pad(cd, ((w // 2, w // 2), (0, 0)), mode='edge')
+    cd = np.stack([np.convolve(pad[:, i], np.ones(w) / w, mode='valid') for i in range(2)], axis=1)
     X = np.zeros((N + 1, 9))
-    X[:, 0:2] = cxy
-    sm = lambda v: np.convolve(v, np.ones(9) / 9, mode='valid')
-    X[:, 1] += sm(rng.normal(0, 0.005, N + 9))
-    X[:, 2] = com_z + sm(rng.normal(0, 0.003, N + 9))
-    vel = np.zeros((N + 1, 3))
-    vel[:-1] = np.diff(X[:, 0:3], axis=0) / conf.dt
-    vel[-1] = vel[-2]
-    X[:, 3:6] = mass * vel
-    kn = rng.normal(0, 0.01, (N + 9, 3))
-    X[:, 6:9] = np.stack([sm(kn[:, i]) for i in range(3)], axis=1)
+    X[0, 0:2] = cd[0]
+    X[0, 2] = com_z
+    g = -gravity
+    kp, kd = 40.0, 12.0
+    for k in range(N):
+        x = X[k]
+        c, v = x[0:3], x[3:6] / mass
+        a_ff = (cd[k + 2] - 2 * cd[k + 1] + cd[k]) / dt ** 2 if k + 2 <= N + 1 else np.zeros(2)
+        axy = a_ff + kp * (cd[k] - c[:2]) + kd * ((cd[k + 1] - cd[k]) / dt - v[:2])
+        az = kp * (com_z - c[2]) - kd * v[2]
+        act = np.nonzero(logic[k])[0]
+        fz = mass * (g + az) / len(act)
+        fxy = mass * axy / len(act)
+        lim = 0.25 * fz
+        nrm = np.linalg.norm(fxy)
+        if nrm > lim:
+            fxy = fxy * lim / nrm
+        F = np.zeros(9)
+        F[0:3] = v
+        F[5] = mass * gravity
+        for i in act:
+            f = np.array([fxy[0], fxy[1], fz])
+            F[3:6] += f
+            F[6:9] += np.cross(pos[k, i] - c, f)
+        X[k + 1] = x + dt * F
+    sm = lambda v_: np.convolve(v_, np.ones(9) / 9, mode='valid')
+    env = np.sin(np.pi * np.arange(N + 1) / N) ** 2
+    X[:, 0:3] += env[:, None] * np.stack([sm(rng.normal(0, 0.002, N + 9)) for _ in range(3)], axis=1)
+    X[:, 3:6] += mass * env[:, None] * np.stack([sm(rng.normal(0, 0.02, N + 9)) for _ in range(3)], axis=1)
+    X[:, 6:9] += env[:, None] * np.stack([sm(rng.normal(0, 0.01, N + 9)) for _ in range(3)], axis=1)
     return X
 
 
@@ -118,7 +144,7 @@ def make_batch(cfg, N, B, stochastic=False, seed_offset=0, mixed=None):
         rng = np.random.default_rng(1000 * CONFIGS[names[c]][1] + b + seed_offset)
         lg, ps, rt = contact_plan(conf, N, rng)
         logic[b], pos[b], rot[b] = lg, ps, rt
-        Xbar[b] = warm_start(conf, lg, ps, rng, params[c].mass, com_z)
+        Xbar[b] = warm_start(conf, lg, ps, rng, params[c].mass, com_z, params[c].gravity, robot)
         Ubar[b] = warm_start_controls(lg, params[c].mass, params[c].gravity, nu)
         cid[b] = c
     pb = ProblemBatch(robot, N, nc, nu, logic, pos, rot, Xbar, Ubar, cid, params)

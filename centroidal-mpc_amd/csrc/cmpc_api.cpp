@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -78,6 +79,10 @@ struct cmpc_handle_s {
     hipStream_t stream = nullptr;
     hipEvent_t ev[5] = {};
     bool timed = false;
+    // accumulated timing: one 5-event record per cmpc_scp_iterate since cmpc_timing_reset
+    std::vector<std::array<hipEvent_t, 5>> ev_pool;
+    size_t ev_used = 0;
+    bool accumulate = false;
     std::string err;
     cmpc_qp_settings qs{};
     std::vector<cmpc_params> hparams;
@@ -249,8 +254,8 @@ const char *cmpc_last_error(cmpc_handle h) { return h ? h->err.c_str() : "null h
 int cmpc_default_qp_settings(int precision, cmpc_qp_settings *s) {
     if (!s) return -1;
     s->max_iter = precision == CMPC_PREC_F64 ? 60 : 40;
-    s->eps_abs = precision == CMPC_PREC_F64 ? 1e-9 : 1e-5;
-    s->eps_rel = precision == CMPC_PREC_F64 ? 1e-9 : 1e-5;
+    s->eps_abs = precision == CMPC_PREC_F64 ? 1e-10 : 1e-6;
+    s->eps_rel = precision == CMPC_PREC_F64 ? 1e-10 : 1e-6;
     s->step_fraction = 0.99;
     return 0;
 }
@@ -323,6 +328,8 @@ int cmpc_destroy(cmpc_handle h) {
     for (void *p : h->allocs) (void)hipFree(p);
     for (auto &e : h->ev)
         if (e) (void)hipEventDestroy(e);
+    for (auto &a : h->ev_pool)
+        for (auto &e : a) (void)hipEventDestroy(e);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return 0;
@@ -402,16 +409,25 @@ int cmpc_accept(cmpc_handle h, int fixed_iters) { return guard(h, [&] { phase(h,
 int cmpc_scp_iterate(cmpc_handle h, int fixed_iters) {
     return guard(h, [&] {
         const int oa = fixed_iters ? 0 : 1;
-        HIPCHK(hipEventRecord(h->ev[0], h->stream));
+        hipEvent_t *ev = h->ev;
+        if (h->accumulate) {
+            if (h->ev_used == h->ev_pool.size()) {
+                std::array<hipEvent_t, 5> a;
+                for (auto &e : a) HIPCHK(hipEventCreate(&e));
+                h->ev_pool.push_back(a);
+            }
+            ev = h->ev_pool[h->ev_used++].data();
+        }
+        HIPCHK(hipEventRecord(ev[0], h->stream));
         phase(h, 0, oa);
-        HIPCHK(hipEventRecord(h->ev[1], h->stream));
+        HIPCHK(hipEventRecord(ev[1], h->stream));
         phase(h, 1, oa);
-        HIPCHK(hipEventRecord(h->ev[2], h->stream));
+        HIPCHK(hipEventRecord(ev[2], h->stream));
         phase(h, 2, oa);
-        HIPCHK(hipEventRecord(h->ev[3], h->stream));
+        HIPCHK(hipEventRecord(ev[3], h->stream));
         phase(h, 3, oa);
-        HIPCHK(hipEventRecord(h->ev[4], h->stream));
-        h->timed = true;
+        HIPCHK(hipEventRecord(ev[4], h->stream));
+        if (!h->accumulate) h->timed = true;
     });
 }
 
@@ -660,6 +676,44 @@ int cmpc_get_timing(cmpc_handle h, cmpc_timing *t) {
         for (int i = 0; i < 4; ++i) HIPCHK(hipEventElapsedTime(&ms[i], h->ev[i], h->ev[i + 1]));
         t->linearize_ms = ms[0]; t->assemble_ms = ms[1]; t->qp_ms = ms[2]; t->accept_ms = ms[3];
         HIPCHK(hipEventElapsedTime(&t->total_ms, h->ev[0], h->ev[4]));
+    });
+}
+
+int cmpc_timing_begin(cmpc_handle h) {
+    return guard(h, [&] {
+        h->accumulate = true;
+        h->ev_used = 0;
+    });
+}
+
+int cmpc_timing_end(cmpc_handle h, cmpc_timing *t, int *n_iterations) {
+    return guard(h, [&] {
+        need(t != nullptr, "null timing");
+        need(h->accumulate, "cmpc_timing_begin was not called");
+        h->accumulate = false;
+        cmpc_timing acc{0, 0, 0, 0, 0};
+        for (size_t i = 0; i < h->ev_used; ++i) {
+            auto &ev = h->ev_pool[i];
+            HIPCHK(hipEventSynchronize(ev[4]));
+            float ms[4], tot;
+            for (int p = 0; p < 4; ++p) HIPCHK(hipEventElapsedTime(&ms[p], ev[p], ev[p + 1]));
+            HIPCHK(hipEventElapsedTime(&tot, ev[0], ev[4]));
+            acc.linearize_ms += ms[0]; acc.assemble_ms += ms[1]; acc.qp_ms += ms[2]; acc.accept_ms += ms[3];
+            acc.total_ms += tot;
+        }
+        *t = acc;
+        if (n_iterations) *n_iterations = (int)h->ev_used;
+    });
+}
+
+int cmpc_get_qp_iterations_total(cmpc_handle h, int64_t *total) {
+    return guard(h, [&] {
+        need(total != nullptr, "null output");
+        std::vector<int32_t> it(h->B);
+        from_dev_raw(h, it.data(), h->qp_iters, (size_t)h->B * 4);
+        int64_t s = 0;
+        for (int v : it) s += v;
+        *total = s;
     });
 }
 

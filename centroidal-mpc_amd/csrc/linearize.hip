@@ -28,7 +28,10 @@ __device__ __forceinline__ void wmm(T *Cm, const T *Am, const T *Bm, int m, int 
             const T b = tb ? Bm[j * k + q] : Bm[q * n + j];
             acc = fma(a, b, acc);
         }
-        Cm[e] = alpha * acc + (Cadd ? Cadd[e] : beta_c * Cm[e]);
+        T v = alpha * acc;
+        if (Cadd) v += Cadd[e];
+        else if (beta_c != T(0)) v += beta_c * Cm[e];   // never read an uninitialized C when beta = 0
+        Cm[e] = v;
     }
     wave_sync();
 }

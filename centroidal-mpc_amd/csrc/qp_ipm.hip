@@ -528,9 +528,10 @@ template <typename T> __device__ void seq_factor(T *Sd, T *So, int NB, T *sh) {
             Lm[e] = v;
         }
         wave_sync();
-        // Cholesky (lower) in Lm
+        // Cholesky (lower) in Lm, with a pivot floor (modified Cholesky): near the solution of
+        // a degenerate QP the last Schur blocks are differences of O(M) numbers
         for (int c = 0; c < 9; ++c) {
-            const T d = sqrt(Lm[c * 9 + c]);
+            const T d = sqrt(fmax(Lm[c * 9 + c], T(1e-13) * Sj[c * 9 + c]));
             const T id = T(1) / d;
             wave_sync();
             if (lane > c && lane < 9) Lm[lane * 9 + c] *= id;
@@ -778,7 +779,7 @@ template <typename T, int ROBOT> __device__ T mu_after(const Ctx<T, ROBOT> &C, i
     return acc;
 }
 
-template <typename T, int ROBOT> __device__ void phase_update(const Ctx<T, ROBOT> &C, int k, T a) {
+template <typename T, int ROBOT> __device__ void phase_update(const Ctx<T, ROBOT> &C, int k, T a, bool affine = false) {
     constexpr int NI = Rows<ROBOT>::NI;
     const int N = C.N;
     T *x = C.var_x(k);
@@ -795,11 +796,39 @@ template <typename T, int ROBOT> __device__ void phase_update(const Ctx<T, ROBOT
     for (int i = 0; i < 9; ++i) nu[(size_t)(1 + k) * 9 + i] += a * dnu[(size_t)(1 + k) * 9 + i];   // k<N: dyn k; k==N: final
     if (k == 0) for (int i = 0; i < 9; ++i) nu[i] += a * dnu[i];
     T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
-    const T *ds = C.ws + C.L.ds + (size_t)k * NI, *dl = C.ws + C.L.dl + (size_t)k * NI;
+    const T *ds = C.ws + (affine ? C.L.dsa : C.L.ds) + (size_t)k * NI;
+    const T *dl = C.ws + (affine ? C.L.dla : C.L.dl) + (size_t)k * NI;
     for (int r = 0; r < NI; ++r) {
         if (!C.present(k, r)) continue;
         s[r] += a * ds[r];
         lm[r] += a * dl[r];
+    }
+}
+
+// initialization step: full Newton step for z and nu; s = h - gz at the new z; lambda += dlambda.
+// vmax receives (max -s, max -lambda) over this knot's rows.
+template <typename T, int ROBOT> __device__ void phase_init_step(const Ctx<T, ROBOT> &C, int k, T (&vmax)[2]) {
+    constexpr int NI = Rows<ROBOT>::NI;
+    phase_update<T, ROBOT>(C, k, T(1), true);   // z, nu, lambda: full affine step; s recomputed below
+    const int N = C.N;
+    const T *x = C.var_x(k);
+    const T t = C.ws[C.L.t + k];
+    const T *u = (k < N) ? C.var_u(k) : nullptr;
+    T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
+    for (int r = 0; r < NI; ++r) {
+        if (!C.present(k, r)) continue;
+        s[r] = -C.gz(k, r, x, t, u, true);
+        vmax[0] = fmax(vmax[0], -s[r]);
+        vmax[1] = fmax(vmax[1], -lm[r]);
+    }
+}
+template <typename T, int ROBOT> __device__ void phase_init_shift(const Ctx<T, ROBOT> &C, int k, T sh_s, T sh_l) {
+    constexpr int NI = Rows<ROBOT>::NI;
+    T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
+    for (int r = 0; r < NI; ++r) {
+        if (!C.present(k, r)) continue;
+        s[r] += sh_s;
+        lm[r] += sh_l;
     }
 }
 
@@ -822,7 +851,7 @@ __global__ void __launch_bounds__(NT) k_qp_ipm(DevBuf<T> d, int only_active, int
     C.cw = d.cw[b];
     C.beta = C.prm->dt / C.prm->mass;
     C.ws = d.ws + (size_t)b * d.ws_stride;
-    // ---- initial point: z = (xbar, ubar, 0), nu = 0, s = max(h - gz, 1), lambda = 1
+    // ---- starting point of the initialization step: z = (xbar, ubar, 0), nu = 0, s = lambda = 1
     for (int k = tid; k < K1; k += NT) {
         T *x = C.var_x(k);
         for (int i = 0; i < 9; ++i) x[i] = C.xbar[(size_t)k * 9 + i];
@@ -831,32 +860,40 @@ __global__ void __launch_bounds__(NT) k_qp_ipm(DevBuf<T> d, int only_active, int
         if (k < N) { T *u = C.var_u(k); for (int i = 0; i < NU; ++i) u[i] = ubar[i]; }
         T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
         for (int r = 0; r < NI; ++r) {
-            if (C.present(k, r)) {
-                s[r] = fmax(-C.gz(k, r, x, T(0), k < N ? ubar : nullptr, true), T(1));
-                lm[r] = T(1);
-            } else { s[r] = T(1); lm[r] = T(0); }
+            s[r] = T(1);
+            lm[r] = C.present(k, r) ? T(1) : T(0);
         }
         T *dsa = C.ws + C.L.dsa + (size_t)k * NI, *dla = C.ws + C.L.dla + (size_t)k * NI;
         for (int r = 0; r < NI; ++r) { dsa[r] = T(0); dla[r] = T(0); }
     }
     for (int e = tid; e < NB * 9; e += NT) C.ws[C.L.nu + e] = T(0);
     __syncthreads();
-    int status = CMPC_QP_MAX_ITER, it = 0;
-    T mu_hist = T(1e300);
-    for (it = 0; it < max_iter; ++it) {
+    int status = CMPC_QP_MAX_ITER, it = 0, stall = 0;
+    T mu_prev = T(-1);
+    // it == 0 is the initialization step (CVXOPT-style): one full Newton step from
+    // s = lambda = 1 gives an equality-feasible least-squares start; s and lambda are then
+    // shifted by (1 + max violation) where negative.
+    for (it = 0; it <= max_iter; ++it) {
+        const bool init = (it == 0);
         Norms<T, ROBOT> nm{0, 0, 0, 0, 0, 0, 0, 0};
         for (int k = tid; k < K1; k += NT) phase_residual<T, ROBOT>(C, k, nm);
         T mx[6] = {nm.prim, nm.dual, nm.comp, nm.sp, nm.sd, nm.lmax};
         block_reduce<T, NT, 6, 1>(mx, red);
         T sm2[2] = {nm.mu, nm.cnt};
         block_reduce<T, NT, 2, 0>(sm2, red);
-        const T prim = mx[0], dual = mx[1], comp = mx[2], sp = mx[3], sdd = mx[4], lmax = mx[5];
+        const T prim = mx[0], dual = mx[1], comp = mx[2], sp = mx[3], sdd = mx[4];
         const T mu = sm2[0] / fmax(sm2[1], T(1));
-        if (!(prim == prim) || !(dual == dual) || !(mu == mu)) { status = CMPC_QP_NONFINITE; break; }
         const T ep = eps_abs + eps_rel * sp, ed = eps_abs + eps_rel * sdd;
-        const T ec = eps_abs + eps_rel * fmax(T(1), lmax) * T(1e-3);
-        if (prim <= ep && dual <= ed && comp <= ec) { status = 1; break; }
-        mu_hist = mu;
+        const T merit = fmax(prim / ep, fmax(dual / ed, comp / ed));
+        if (!(merit == merit) || !(mu == mu)) { status = CMPC_QP_NONFINITE; break; }
+        if (!init) {
+            if (merit <= T(1)) { status = 1; break; }
+            // stall guard: mu not decreasing for 3 iterations while within 1e3x of tolerance
+            stall = (mu_prev >= T(0) && mu >= T(0.5) * mu_prev) ? stall + 1 : 0;
+            mu_prev = mu;
+            if (stall >= 3 && merit <= T(1e3)) { status = 1; break; }
+        }
+        if (it == max_iter) break;
         // ---- factorization
         for (int k = tid; k < K1; k += NT) phase_factor<T, ROBOT>(C, k);
         __syncthreads();
@@ -878,6 +915,7 @@ __global__ void __launch_bounds__(NT) k_qp_ipm(DevBuf<T> d, int only_active, int
             for (int k = tid; k < K1; k += NT) am[0] = fmin(am[0], phase_dz<T, ROBOT>(C, k, corr, sigma_mu));
             block_reduce<T, NT, 1, 2>(am, red);
             alpha = am[0];
+            if (init) break;
             if (corr == 0) {
                 T ma[1] = {T(0)};
                 for (int k = tid; k < K1; k += NT) ma[0] += mu_after<T, ROBOT>(C, k, alpha);
@@ -887,11 +925,20 @@ __global__ void __launch_bounds__(NT) k_qp_ipm(DevBuf<T> d, int only_active, int
                 sigma_mu = sg * sg * sg * mu;
             }
         }
+        if (init) {
+            T vmax[2] = {T(-1e300), T(-1e300)};
+            for (int k = tid; k < K1; k += NT) phase_init_step<T, ROBOT>(C, k, vmax);
+            block_reduce<T, NT, 2, 1>(vmax, red);
+            const T sh_s = vmax[0] >= T(0) ? T(1) + vmax[0] : T(0);
+            const T sh_l = vmax[1] >= T(0) ? T(1) + vmax[1] : T(0);
+            for (int k = tid; k < K1; k += NT) phase_init_shift<T, ROBOT>(C, k, sh_s, sh_l);
+            __syncthreads();
+            continue;
+        }
         alpha = fmin(T(1), eta * alpha);
         for (int k = tid; k < K1; k += NT) phase_update<T, ROBOT>(C, k, alpha);
         __syncthreads();
     }
-    (void)mu_hist;
     // ---- outputs: solution and multipliers
     for (int k = tid; k < K1; k += NT) {
         const T *x = C.var_x(k);

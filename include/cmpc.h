@@ -80,8 +80,8 @@ typedef struct {
 /* QP solver settings (defaults by cmpc_default_qp_settings) */
 typedef struct {
     int32_t max_iter;       /* interior-point iterations (default 60) */
-    double eps_abs;         /* absolute tolerance (fp64 default 1e-9) */
-    double eps_rel;         /* relative tolerance (fp64 default 1e-9) */
+    double eps_abs;         /* absolute tolerance (fp64 default 1e-10, fp32 1e-6) */
+    double eps_rel;         /* relative tolerance (fp64 default 1e-10, fp32 1e-6) */
     double step_fraction;   /* fraction-to-boundary (default 0.99) */
 } cmpc_qp_settings;
 
@@ -131,6 +131,12 @@ int cmpc_get_solution(cmpc_handle h, double *X, double *U, double *K, double *Si
 int cmpc_get_iteration_log(cmpc_handle h, double *tr_norm, double *rho, int32_t *qp_status,
                            int32_t *qp_iters, int32_t *decision);
 int cmpc_get_timing(cmpc_handle h, cmpc_timing *t);
+/* Accumulate per-phase HIP-event timings of every cmpc_scp_iterate between begin and end
+ * (no host synchronization inside the region; end synchronizes and sums). */
+int cmpc_timing_begin(cmpc_handle h);
+int cmpc_timing_end(cmpc_handle h, cmpc_timing *t, int *n_iterations);
+/* Sum over problems of the interior-point iterations of the last QP solve. */
+int cmpc_get_qp_iterations_total(cmpc_handle h, int64_t *total);
 
 #ifdef __cplusplus
 }

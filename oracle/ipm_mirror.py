@@ -45,11 +45,24 @@ class StructQP:
                         fmask=logic.astype(bool), foot_range=foot_range, Xbar=Xbar, Ubar=Ubar)
 
 
+def _chol_floor(S, floor):
+    """Cholesky with a pivot floor (modified Cholesky): near the solution of a degenerate QP
+    the last Schur blocks are differences of O(M) numbers and may lose positivity by rounding."""
+    n = S.shape[0]
+    L = np.zeros_like(S)
+    for c in range(n):
+        d2 = S[c, c] - L[c, :c] @ L[c, :c]
+        d = np.sqrt(max(d2, floor[c]))
+        L[c, c] = d
+        L[c + 1:, c] = (S[c + 1:, c] - L[c + 1:, :c] @ L[c, :c]) / d
+    return L
+
+
 def _fslot(qp):
     return 0 if qp.robot == 'solo12' else 2
 
 
-def solve(qp, eps=1e-9, max_iter=60, eta=0.99, verbose=False):
+def solve(qp, eps=1e-10, max_iter=60, eta=0.99, verbose=False, reg=0.0, piv_floor=1e-13):
     N, nc, nu, nupc = qp.N, qp.nc, qp.nu, qp.nupc
     fo = _fslot(qp)
     talos = qp.robot != 'solo12'
@@ -118,7 +131,14 @@ def solve(qp, eps=1e-9, max_iter=60, eta=0.99, verbose=False):
     e_rhs = np.zeros((N + 2, 9)); e_rhs[0] = qp.x0; e_rhs[1:N + 1] = qp.r; e_rhs[N + 1] = qp.xN
     it = 0; status = -2
     hist = []
-    for it in range(1, max_iter + 1):
+    s = [mk * 1.0 + (1 - mk) for mk in masks]
+    lam = [mk * 1.0 for mk in masks]
+    stall = 0; mu_prev = None
+    for it in range(0, max_iter + 1):
+        # iteration 0 is the initialization step (CVXOPT-style): one full Newton step from
+        # s = lambda = 1 (an equality-constrained least-squares start), then s and lambda are
+        # shifted to be >= 1 where negative.
+        init = it == 0
         # ---- residuals ----
         gx, gt, gu = GT(lam)
         ex, eu = ET(nu_)
@@ -138,7 +158,17 @@ def solve(qp, eps=1e-9, max_iter=60, eta=0.99, verbose=False):
         hist.append((it, prim, dual, comp, mu_))
         if verbose:
             print('it %2d prim %.2e dual %.2e comp %.2e mu %.2e' % (it, prim, dual, comp, mu_))
-        if prim <= eps * scale_p and dual <= eps * scale_d and comp <= eps * scale_d:
+        merit = max(prim / (eps * scale_p), dual / (eps * scale_d), comp / (eps * scale_d))
+        if not (merit == merit):
+            status = -10
+            break
+        if not init and merit <= 1.0:
+            status = 1
+            break
+        # stall guard: mu no longer decreasing for 3 iterations while within 1e3x of tolerance
+        stall = stall + 1 if (not init and mu_prev is not None and mu_ >= 0.5 * mu_prev) else 0
+        mu_prev = None if init else mu_
+        if stall >= 3 and merit <= 1e3:
             status = 1
             break
         # ---- factorization ----
@@ -183,9 +213,13 @@ def solve(qp, eps=1e-9, max_iter=60, eta=0.99, verbose=False):
         So[N] = -Mfull[N]
         # block Cholesky: Lc[j] lower, Lo[j] = S_{j+1,j} Lc[j]^-T
         Lc = np.zeros_like(Sd); Lo = np.zeros_like(So)
+        # tiny diagonal regularization of each Schur block: the last blocks are differences of
+        # O(M) numbers once the forces are pinned by active rows (cancellation), see DESIGN.md
+        for j in range(N + 2):
+            Sd[j] += reg * np.trace(Sd[j]) / 9 * np.eye(9)
         Sh = Sd[0].copy()
         for j in range(N + 2):
-            Lc[j] = np.linalg.cholesky(Sh)
+            Lc[j] = _chol_floor(Sh, piv_floor * np.diag(Sd[j]))
             if j < N + 1:
                 Lo[j] = np.linalg.solve(Lc[j], So[j]).T        # (S_{j,j+1})^T Lc^-T
                 Sh = Sd[j + 1] - Lo[j] @ Lo[j].T
@@ -244,6 +278,16 @@ def solve(qp, eps=1e-9, max_iter=60, eta=0.99, verbose=False):
 
         rc_aff = [si * li * mk for si, li, mk in zip(s, lam, masks)]
         dx, dt_, du, dnu, dl, ds = newton(rc_aff)
+        if init:
+            x = x + dx; t = t + dt_; u = u + du; nu_ = nu_ + dnu
+            vals = ineq_val(x, u, t)
+            s_new = [-v * mk for v, mk in zip(vals, masks)]
+            l_new = [(li + dli) * mk for li, dli, mk in zip(lam, dl, masks)]
+            ap = max(float(-np.min(si[mk > 0])) for si, mk in zip(s_new, masks))
+            ad = max(float(-np.min(li[mk > 0])) for li, mk in zip(l_new, masks))
+            s = [np.where(mk > 0, si + (1 + ap if ap >= 0 else 0), 1.0) for si, mk in zip(s_new, masks)]
+            lam = [(li + (1 + ad if ad >= 0 else 0)) * mk for li, mk in zip(l_new, masks)]
+            continue
         a_aff = min(min(max_step(si, dsi, mk) for si, dsi, mk in zip(s, ds, masks)),
                     min(max_step(li, dli, mk) for li, dli, mk in zip(lam, dl, masks)))
         mu_aff = sum(((si + a_aff * dsi) * (li + a_aff * dli) * mk).sum()

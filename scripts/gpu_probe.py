@@ -17,6 +17,7 @@ s = Solver(pb.robot, N, B, prec)
 s.upload(pb)
 t0 = time.time(); s.linearize(); s.synchronize(); print('linearize %.3fs' % (time.time() - t0), flush=True)
 lin = s.linearization()
+print('NaN counts K', np.isnan(lin['K']).sum(), 'Sigma', np.isnan(lin['Sigma']).sum(), 'K[0,0,:3,:3]', lin['K'][0,0,:3,:3], flush=True)
 for b in range(B):
     prob = pb.oracle_problem(b); prm = prob['prm']
     td = M.compute_trajectory_data(prob['Xbar'], prob['Ubar'], prob['logic'], prob['pos'], prob['rot'], prm)
@@ -48,7 +49,7 @@ for b in range(B):
     qp = IM.StructQP.from_arrays(N, pb.robot, pb.nc, p.Wx, p.Wu, pb.Xbar[b], pb.Ubar[b], td['f_x'], td['f_u'],
                                  td['dynamics'].T, pb.logic[b], pb.rot[b], p.mu, 100., 100., p.tracking,
                                  foot_range=p.foot_range)
-    sol = IM.solve(qp, eps=1e-12)
+    sol = IM.solve(qp, eps=1e-10)
     zm = IM.to_z(qp, sol)
     n_xu = 9 * (N + 1) + 12 * N
     print('b', b, 'kkt prim %.2e dual %.2e compl %.2e sign %.2e | mirror iters %d, |z-zm| %.2e (rel %.2e)' % (
