@@ -10,7 +10,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libcmpc.so')
+LIB_PATH = os.path.join(_HERE, 'libcmpc_diag.so' if os.environ.get('CMPC_LIB_VARIANT') == 'diag' else 'libcmpc.so')
 
 ROBOTS = {'solo12': 0, 'TALOS': 1}
 PREC = {'fp64': 0, 'float64': 0, 'f64': 0, 'fp32': 1, 'float32': 1, 'f32': 1}
@@ -50,7 +50,7 @@ EXPORTS = ['cmpc_create', 'cmpc_destroy', 'cmpc_last_error', 'cmpc_version', 'cm
            'cmpc_qp_solve', 'cmpc_accept', 'cmpc_scp_iterate', 'cmpc_solve_scp', 'cmpc_synchronize',
            'cmpc_get_linearization', 'cmpc_qp_sizes', 'cmpc_export_qp', 'cmpc_get_qp_solution',
            'cmpc_get_solution', 'cmpc_get_iteration_log', 'cmpc_get_timing', 'cmpc_timing_begin',
-           'cmpc_timing_end', 'cmpc_get_qp_iterations_total']
+           'cmpc_timing_end', 'cmpc_get_qp_iterations_total', 'cmpc_debug_stamps']
 
 _lib = None
 
@@ -94,6 +94,7 @@ def load():
         'cmpc_timing_begin': (i32, [h]),
         'cmpc_timing_end': (i32, [h, P(Timing), P(ctypes.c_int)]),
         'cmpc_get_qp_iterations_total': (i32, [h, P(ctypes.c_int64)]),
+        'cmpc_debug_stamps': (i32, [h, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -291,3 +292,8 @@ class Solver:
         v = ctypes.c_int64(0)
         self._chk(self.lib.cmpc_get_qp_iterations_total(self.h, ctypes.byref(v)), 'cmpc_get_qp_iterations_total')
         return int(v.value)
+
+    def debug_stamps(self):
+        out = np.zeros((self.B, 16), np.uint64)
+        self._chk(self.lib.cmpc_debug_stamps(self.h, _ptr(out)), 'cmpc_debug_stamps')
+        return out

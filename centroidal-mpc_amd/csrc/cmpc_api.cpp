@@ -17,7 +17,9 @@
 namespace cmpc {
 template <typename T, int R> __global__ void k_linearize(DevBuf<T>, int);
 template <typename T, int R> __global__ void k_assemble(DevBuf<T>, int);
-template <typename T, int R> __global__ void k_qp_ipm(DevBuf<T>, int, int, T, T, T);
+template <typename T, int R, bool SL> __global__ void k_qp_ipm(DevBuf<T>, int, int, T, T, T);
+size_t ipm_schur_lds_bytes(int N, int prec_bytes);
+size_t ipm_vec_lds_bytes(int N, int prec_bytes);
 template <typename T, int R> __global__ void k_accept(DevBuf<T>, int);
 size_t ipm_workspace_elems(int N, int robot);
 }  // namespace cmpc
@@ -93,7 +95,7 @@ struct cmpc_handle_s {
          *Ubar = nullptr, *f = nullptr, *A = nullptr, *Bu = nullptr, *C = nullptr, *K = nullptr, *Sig = nullptr,
          *Acl = nullptr, *Qw = nullptr, *stage = nullptr, *cw = nullptr, *xs = nullptr, *us = nullptr, *ts = nullptr,
          *nus = nullptr, *lams = nullptr, *qp_status = nullptr, *qp_iters = nullptr, *ws = nullptr, *scp = nullptr,
-         *Xacc = nullptr, *Uacc = nullptr, *Kacc = nullptr, *Sacc = nullptr;
+         *Xacc = nullptr, *Uacc = nullptr, *Kacc = nullptr, *Sacc = nullptr, *stamps = nullptr;
 
     size_t esz() const { return prec == CMPC_PREC_F64 ? 8 : 4; }
     void *dalloc(size_t bytes) {
@@ -115,6 +117,7 @@ struct cmpc_handle_s {
         d.qp_status = (int32_t *)qp_status; d.qp_iters = (int32_t *)qp_iters;
         d.ws = (T *)ws; d.ws_stride = ws_stride; d.scp = (ScpState *)scp;
         d.Xacc = (T *)Xacc; d.Uacc = (T *)Uacc; d.Kacc = (T *)Kacc; d.Sacc = (T *)Sacc;
+        d.stamps = (unsigned long long *)stamps;
         return d;
     }
 };
@@ -204,10 +207,23 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
                            only_active);
         break;
     }
-    case 2:
-        hipLaunchKernelGGL((k_qp_ipm<T, R>), dim3(B), dim3(256), 0, h->stream, d, only_active, h->qs.max_iter,
-                           T(h->qs.eps_abs), T(h->qs.eps_rel), T(h->qs.step_fraction));
+    case 2: {
+        // Schur blocks in LDS when they fit beside the kernel's static LDS (one workgroup per CU)
+        const size_t vec = ipm_vec_lds_bytes(h->N, (int)sizeof(T));
+        const size_t lds = vec + ipm_schur_lds_bytes(h->N, (int)sizeof(T));
+        if (lds <= 150 * 1024) {
+            HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_qp_ipm<T, R, true>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            hipLaunchKernelGGL((k_qp_ipm<T, R, true>), dim3(B), dim3(256), lds, h->stream, d, only_active,
+                               h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), T(h->qs.step_fraction));
+        } else {
+            HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_qp_ipm<T, R, false>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)vec));
+            hipLaunchKernelGGL((k_qp_ipm<T, R, false>), dim3(B), dim3(256), vec, h->stream, d, only_active,
+                               h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), T(h->qs.step_fraction));
+        }
         break;
+    }
     case 3:
         hipLaunchKernelGGL((k_accept<T, R>), dim3(B), dim3(256), 0, h->stream, d, only_active ? 0 : 1);
         break;
@@ -254,8 +270,8 @@ const char *cmpc_last_error(cmpc_handle h) { return h ? h->err.c_str() : "null h
 int cmpc_default_qp_settings(int precision, cmpc_qp_settings *s) {
     if (!s) return -1;
     s->max_iter = precision == CMPC_PREC_F64 ? 60 : 40;
-    s->eps_abs = precision == CMPC_PREC_F64 ? 1e-10 : 1e-6;
-    s->eps_rel = precision == CMPC_PREC_F64 ? 1e-10 : 1e-6;
+    s->eps_abs = precision == CMPC_PREC_F64 ? 1e-11 : 1e-6;
+    s->eps_rel = precision == CMPC_PREC_F64 ? 1e-11 : 1e-6;
     s->step_fraction = 0.99;
     return 0;
 }
@@ -310,6 +326,7 @@ int cmpc_create(cmpc_handle *out, int device, int robot, int N, int max_batch, i
         h->Uacc = h->dalloc(Bm * N * NU * e);
         h->Kacc = h->dalloc(Bm * N * NU * 9 * e);
         h->Sacc = h->dalloc(Bm * K1 * 81 * e);
+        h->stamps = h->dalloc(Bm * 16 * 8);
         HIPCHK(hipStreamSynchronize(h->stream));
     });
     if (rc != 0) {
@@ -714,6 +731,13 @@ int cmpc_get_qp_iterations_total(cmpc_handle h, int64_t *total) {
         int64_t s = 0;
         for (int v : it) s += v;
         *total = s;
+    });
+}
+
+int cmpc_debug_stamps(cmpc_handle h, uint64_t *out) {
+    return guard(h, [&] {
+        need(out != nullptr, "null output");
+        from_dev_raw(h, out, h->stamps, (size_t)h->B * 16 * 8);
     });
 }
 

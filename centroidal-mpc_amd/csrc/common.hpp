@@ -81,6 +81,7 @@ template <typename T> struct DevBuf {
     size_t ws_stride;               // elements per problem
     // SCP
     ScpState *scp;
+    unsigned long long *stamps;     // (B,16) per-phase cycle counters (diagnostic builds only)
     T *Xacc, *Uacc, *Kacc, *Sacc;   // accepted solution (B,N+1,9) (B,N,NU) (B,N,108) (B,N+1,81)
 };
 

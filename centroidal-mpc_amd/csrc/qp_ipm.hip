@@ -22,6 +22,9 @@ namespace cmpc {
 
 constexpr int NT = 256;
 constexpr int FU = 34;   // per-contact factor record: Gw 12 | Kinv 10 | F 6 | Winvd 6
+// per-knot (x, t) factor record: 1/Wx[0:6] | M_LL packed 6 | chol(K_TR) packed 36 | z1 = L^-1 1 (8) |
+// den | D_slack  (K_TR = D_TR^-1 + G_L W_L^-1 G_L', see phase_factor)
+constexpr int FX = 64, FX_ML = 6, FX_L = 12, FX_Z1 = 48, FX_DEN = 56, FX_DSL = 57;
 
 // Workspace offsets (elements) for one problem.
 struct WsLayout {
@@ -33,7 +36,7 @@ struct WsLayout {
         auto take = [&](size_t n) { size_t r = o; o += (n + 7) & ~size_t(7); return r; };
         s = take(K1 * NI); l = take(K1 * NI); x = take(K1 * 9); u = take(N * NU); t = take(K1);
         nu = take(NB * 9); rdx = take(K1 * 9); rdt = take(K1); rdu = take(N * NU); rde = take(NB * 9);
-        rdi = take(K1 * NI); facx = take(K1 * 16); facu = take((size_t)N * NC * FU); Sd = take(NB * 81);
+        rdi = take(K1 * NI); facx = take(K1 * FX); facu = take((size_t)N * NC * FU); Sd = take(NB * 81);
         So = take((N + 1) * 81); wx = take(K1 * 9); wt = take(K1); wu = take(N * NU); rhs = take(NB * 9);
         dnu = take(NB * 9); dx = take(K1 * 9); dt = take(K1); du = take(N * NU); ds = take(K1 * NI);
         dl = take(K1 * NI); dsa = take(K1 * NI); dla = take(K1 * NI);
@@ -112,6 +115,9 @@ template <typename T, int ROBOT> struct Ctx {
     T cw, beta;
     T *ws;
     WsLayout L;
+    T *Sd, *So;           // Schur blocks: LDS-resident when they fit (SL), else workspace
+    T dcap;               // cap on D = lambda/s for the CoP rows (D-form, folded into W_cop)
+    __device__ T Dform(T l, T s_) const { return fmin(l / s_, dcap); }
 
     __device__ const T *st(int k) const { return stage + (size_t)k * S::SIZE; }
     __device__ bool present(int k, int row) const {
@@ -220,6 +226,27 @@ template <typename T> __device__ void inv4spd(T (&a)[4][4], T *out) {
 }
 __device__ __forceinline__ int p4(int i, int j) { if (i < j) { int t = i; i = j; j = t; } return i * (i + 1) / 2 + j; }
 
+// relative floor on D^-1 in the push-through blocks (K = D^-1 + G W^-1 G')
+template <typename T> constexpr double KFLOOR = sizeof(T) == 8 ? 1e-12 : 1e-6;
+
+// in-place Cholesky of an 8x8 SPD matrix, packed lower (row j, col q <= j at j(j+1)/2 + q), with
+// a pivot floor relative to the original diagonal
+template <typename T> __device__ void chol8(T (&a)[36]) {
+    for (int j = 0; j < 8; ++j) {
+        const T d0 = a[j * (j + 1) / 2 + j];
+        T d = d0;
+        for (int q = 0; q < j; ++q) d -= a[j * (j + 1) / 2 + q] * a[j * (j + 1) / 2 + q];
+        d = sqrt(fmax(d, T(KFLOOR<T>) * d0));
+        a[j * (j + 1) / 2 + j] = d;
+        const T id = T(1) / d;
+        for (int i = j + 1; i < 8; ++i) {
+            T v = a[i * (i + 1) / 2 + j];
+            for (int q = 0; q < j; ++q) v -= a[i * (i + 1) / 2 + q] * a[j * (j + 1) / 2 + q];
+            a[i * (i + 1) / 2 + j] = v * id;
+        }
+    }
+}
+
 // ------------------------------------------------------------------ phases
 // (1) residuals of knot k; returns norm contributions
 template <typename T, int ROBOT> struct Norms { T prim, dual, comp, mu, sp, sd, lmax, cnt; };
@@ -319,24 +346,54 @@ template <typename T, int ROBOT> __device__ void phase_factor(const Ctx<T, ROBOT
     const int N = C.N;
     const DevParams<T> &P = *C.prm;
     const T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
-    T *fx = C.ws + C.L.facx + (size_t)k * 16;
-    T D[9];
-    for (int r = 0; r < 9; ++r) D[r] = lm[r] / s[r];
-    T A3[3][3], Lt[3] = {0, 0, 0}, tt = D[8];
-    for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) A3[i][j] = (i == j) ? P.Wx[6 + i] : T(0);
-    for (int j = 0; j < 8; ++j) {
-        for (int i = 0; i < 3; ++i) {
-            Lt[i] += C.cw * D[j] * tr_sign<T>(j, i);
-            for (int q = 0; q < 3; ++q) A3[i][q] += D[j] * tr_sign<T>(j, i) * tr_sign<T>(j, q);
+    T *fx = C.ws + C.L.facx + (size_t)k * FX;
+    // (L, t) block in push-through form (no D * r product, no cancellation as rows pin L or t):
+    //   K = D_TR^-1 + Y G_L' (8x8 SPD; Y = G_L W_L^-1; D^-1 floored: at a vertex of the trust
+    //   region more than 3 rows are active and K -> rank 3),  L L' = K,  z1 = L^-1 1,
+    //   den = D_slack + cw^2 |z1|^2,  Z = L^-1 Y,  g = Z' z1,
+    //   M_LL = [Phi^-1]_LL = W_L^-1 - Z'Z + cw^2 g g' / den
+    const T wl[3] = {T(1) / P.Wx[6], T(1) / P.Wx[7], T(1) / P.Wx[8]};
+    const T kfl = T(KFLOOR<T>) * T(8) * (wl[0] + wl[1] + wl[2]);
+    T Lk[36];
+    for (int j = 0; j < 8; ++j)
+        for (int q = 0; q <= j; ++q) {
+            T v = T(0);
+            for (int i = 0; i < 3; ++i) v += tr_sign<T>(j, i) * tr_sign<T>(q, i) * wl[i];
+            if (q == j) v += fmax(s[j] / lm[j], kfl);
+            Lk[j * (j + 1) / 2 + q] = v;
         }
-        tt += C.cw * C.cw * D[j];
+    chol8(Lk);
+    T z1[8], Z[8][3];
+    for (int j = 0; j < 8; ++j) {
+        T a1 = T(1), az[3];
+        for (int i = 0; i < 3; ++i) az[i] = tr_sign<T>(j, i) * wl[i];
+        for (int q = 0; q < j; ++q) {
+            const T l = Lk[j * (j + 1) / 2 + q];
+            a1 -= l * z1[q];
+            for (int i = 0; i < 3; ++i) az[i] -= l * Z[q][i];
+        }
+        const T il = T(1) / Lk[j * (j + 1) / 2 + j];
+        z1[j] = a1 * il;
+        for (int i = 0; i < 3; ++i) Z[j][i] = az[i] * il;
     }
-    for (int i = 0; i < 3; ++i)
-        for (int q = 0; q < 3; ++q) A3[i][q] -= Lt[i] * Lt[q] / tt;
+    T kap = T(0), g[3] = {0, 0, 0};
+    for (int j = 0; j < 8; ++j) {
+        kap += z1[j] * z1[j];
+        for (int i = 0; i < 3; ++i) g[i] += Z[j][i] * z1[j];
+    }
+    const T dsl = lm[8] / s[8];
+    const T den = dsl + C.cw * C.cw * kap;
     for (int i = 0; i < 6; ++i) fx[i] = T(1) / P.Wx[i];
-    inv3sym(A3, fx + 6);
-    fx[12] = Lt[0]; fx[13] = Lt[1]; fx[14] = Lt[2]; fx[15] = tt;
+    for (int i = 0, p = 0; i < 3; ++i)
+        for (int q = 0; q <= i; ++q, ++p) {
+            T zz = T(0);
+            for (int j = 0; j < 8; ++j) zz += Z[j][i] * Z[j][q];
+            fx[FX_ML + p] = (i == q ? wl[i] : T(0)) - zz + C.cw * C.cw * g[i] * g[q] / den;
+        }
+    for (int e = 0; e < 36; ++e) fx[FX_L + e] = Lk[e];
+    for (int j = 0; j < 8; ++j) fx[FX_Z1 + j] = z1[j];
+    fx[FX_DEN] = den;
+    fx[FX_DSL] = dsl;
     if (k >= N) return;
     for (int c = 0; c < NC; ++c) {
         T *fu = C.ws + C.L.facu + ((size_t)k * NC + c) * FU;
@@ -346,7 +403,7 @@ template <typename T, int ROBOT> __device__ void phase_factor(const Ctx<T, ROBOT
         if (ROBOT == 1 && C.logic[k * NC + c]) {
             for (int dd = 0; dd < 2; ++dd) {
                 const int r0 = R_::CP + 4 * c + 2 * dd;
-                fu[28 + dd] = T(1) / (Wc[dd] + lm[r0] / s[r0] + lm[r0 + 1] / s[r0 + 1]);
+                fu[28 + dd] = T(1) / (Wc[dd] + C.Dform(lm[r0], s[r0]) + C.Dform(lm[r0 + 1], s[r0 + 1]));
             }
         }
         const T wi[3] = {T(1) / Wc[FO], T(1) / Wc[FO + 1], T(1) / Wc[FO + 2]};
@@ -361,13 +418,17 @@ template <typename T, int ROBOT> __device__ void phase_factor(const Ctx<T, ROBOT
         T Gw[4][3];
         for (int r = 0; r < 4; ++r)
             for (int q = 0; q < 3; ++q) { Gw[r][q] = cs[S::G + 3 * r + q] * wi[q]; fu[3 * r + q] = Gw[r][q]; }
-        T Km[4][4];
+        T Km[4][4], tr = T(0);
         for (int r = 0; r < 4; ++r)
             for (int q = 0; q < 4; ++q) {
-                T acc = (r == q) ? s[R_::FR + 4 * c + r] / lm[R_::FR + 4 * c + r] : T(0);
+                T acc = T(0);
                 for (int z = 0; z < 3; ++z) acc += Gw[r][z] * cs[S::G + 3 * q + z];
                 Km[r][q] = acc;
             }
+        for (int r = 0; r < 4; ++r) tr += Km[r][r];
+        // floor on D^-1: at a zero force all four pyramid rows are active (K -> rank 3)
+        const T kfloor = T(KFLOOR<T>) * tr + T(sizeof(T) == 8 ? 1e-300 : 1e-37);
+        for (int r = 0; r < 4; ++r) Km[r][r] += fmax(s[R_::FR + 4 * c + r] / lm[R_::FR + 4 * c + r], kfloor);
         T Ki[10];
         inv4spd(Km, Ki);
         for (int q = 0; q < 10; ++q) fu[12 + q] = Ki[q];
@@ -383,18 +444,9 @@ template <typename T, int ROBOT> __device__ void phase_factor(const Ctx<T, ROBOT
     }
 }
 
-// Phi^-1 v for knot k: (vx[9], vt, vu[NU]) -> (ox, ot, ou)
-template <typename T, int ROBOT>
-__device__ void phi_solve(const Ctx<T, ROBOT> &C, int k, const T *vx, T vt, const T *vu, T *ox, T &ot, T *ou) {
+// Phi_u^-1 vu for the control blocks of knot k < N (friction rows in push-through form)
+template <typename T, int ROBOT> __device__ void phi_solve_u(const Ctx<T, ROBOT> &C, int k, const T *vu, T *ou) {
     constexpr int NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
-    const T *fx = C.ws + C.L.facx + (size_t)k * 16;
-    const T tt = fx[15];
-    T w[3];
-    for (int i = 0; i < 3; ++i) w[i] = vx[6 + i] - fx[12 + i] * (vt / tt);
-    for (int i = 0; i < 6; ++i) ox[i] = fx[i] * vx[i];
-    for (int i = 0; i < 3; ++i) ox[6 + i] = sym3(fx + 6, i, 0) * w[0] + sym3(fx + 6, i, 1) * w[1] + sym3(fx + 6, i, 2) * w[2];
-    ot = (vt - (fx[12] * ox[6] + fx[13] * ox[7] + fx[14] * ox[8])) / tt;
-    if (k >= C.N) return;
     for (int c = 0; c < NC; ++c) {
         const T *fu = C.ws + C.L.facu + ((size_t)k * NC + c) * FU;
         const T *vc = vu + NUPC * c;
@@ -405,13 +457,49 @@ __device__ void phi_solve(const Ctx<T, ROBOT> &C, int k, const T *vx, T vt, cons
     }
 }
 
+// local solve of the (L, t) block of knot k (unknowns dL, dt, dlam_TR[8], dlam_slack):
+//   W_L dL + G_L' dlam = vL;  cw 1'dlam - dlam_sl = vt;  G_L dL + cw 1 dt - D^-1 dlam = -rh[0:8];
+//   -dt - D_sl^-1 dlam_sl = -rh[8]
+// dt = (vt + D_sl rh_8 - cw z1'y) / den with y = L^-1 (Y vL + rh);  dlam = L^-T (y + cw dt z1);
+// dL = W_L^-1 (vL - G_L' dlam);  dlam_sl = cw 1'dlam - vt  (the t row of the dual residual)
+template <typename T, int ROBOT>
+__device__ void tr_local(const Ctx<T, ROBOT> &C, int k, const T *vL, T vt, const T *rh, T *dL, T &dt, T *dlt, T &dls) {
+    const T *fx = C.ws + C.L.facx + (size_t)k * FX;
+    const T *Lk = fx + FX_L, *z1 = fx + FX_Z1;
+    const T wl[3] = {T(1) / C.prm->Wx[6], T(1) / C.prm->Wx[7], T(1) / C.prm->Wx[8]};
+    T y[8];
+    for (int j = 0; j < 8; ++j) {
+        T v = rh[j];
+        for (int i = 0; i < 3; ++i) v += tr_sign<T>(j, i) * wl[i] * vL[i];
+        for (int q = 0; q < j; ++q) v -= Lk[j * (j + 1) / 2 + q] * y[q];
+        y[j] = v / Lk[j * (j + 1) / 2 + j];
+    }
+    T zy = T(0);
+    for (int j = 0; j < 8; ++j) zy += z1[j] * y[j];
+    dt = (vt + fx[FX_DSL] * rh[8] - C.cw * zy) / fx[FX_DEN];
+    for (int j = 0; j < 8; ++j) y[j] += C.cw * dt * z1[j];
+    for (int j = 7; j >= 0; --j) {
+        T v = y[j];
+        for (int q = j + 1; q < 8; ++q) v -= Lk[q * (q + 1) / 2 + j] * dlt[q];
+        dlt[j] = v / Lk[j * (j + 1) / 2 + j];
+    }
+    T sl = T(0);
+    for (int j = 0; j < 8; ++j) sl += dlt[j];
+    dls = C.cw * sl - vt;
+    for (int i = 0; i < 3; ++i) {
+        T gl = T(0);
+        for (int j = 0; j < 8; ++j) gl += tr_sign<T>(j, i) * dlt[j];
+        dL[i] = wl[i] * (vL[i] - gl);
+    }
+}
+
 // (3) S blocks owned by knot k
 template <typename T, int ROBOT> __device__ void phase_sblock(const Ctx<T, ROBOT> &C, int k) {
     using S = Stage<ROBOT>;
     constexpr int NC = Robot<ROBOT>::NC;
     const int N = C.N;
     const T beta = C.beta;
-    const T *fx = C.ws + C.L.facx + (size_t)k * 16;
+    const T *fx = C.ws + C.L.facx + (size_t)k * FX;
     auto Mfull = [&](const T *f, int i, int j) -> T {   // M_k entry
         if (i < 6 || j < 6) return (i == j && i < 6) ? f[i] : T(0);
         return sym3(f + 6, i - 6, j - 6);
@@ -433,7 +521,7 @@ template <typename T, int ROBOT> __device__ void phase_sblock(const Ctx<T, ROBOT
         return sym3(f + 6, i - 6, j - 6);
     };
     if (k == 0) {
-        T *Sd = C.ws + C.L.Sd, *So = C.ws + C.L.So;
+        T *Sd = C.Sd, *So = C.So;
         for (int i = 0; i < 9; ++i)
             for (int j = 0; j < 9; ++j) {
                 Sd[i * 9 + j] = Mfull(fx, i, j);
@@ -441,12 +529,12 @@ template <typename T, int ROBOT> __device__ void phase_sblock(const Ctx<T, ROBOT
             }
     }
     if (k == N) {
-        T *Sd = C.ws + C.L.Sd + (size_t)(N + 1) * 81;
+        T *Sd = C.Sd + (size_t)(N + 1) * 81;
         for (int i = 0; i < 9; ++i)
             for (int j = 0; j < 9; ++j) Sd[i * 9 + j] = Mfull(fx, i, j);
         return;
     }
-    const T *fx1 = fx + 16;
+    const T *fx1 = fx + FX;
     const T *w = C.st(k) + S::W;
     const T Wm[3][3] = {{0, -w[2], w[1]}, {w[2], 0, -w[0]}, {-w[1], w[0], 0}};
     T Sm[9][9];
@@ -501,9 +589,9 @@ template <typename T, int ROBOT> __device__ void phase_sblock(const Ctx<T, ROBOT
     // + M_{k+1}
     for (int i = 0; i < 9; ++i)
         for (int j = 0; j < 9; ++j) Sm[i][j] += Mfull(fx1, i, j);
-    T *Sd = C.ws + C.L.Sd + (size_t)(1 + k) * 81;
+    T *Sd = C.Sd + (size_t)(1 + k) * 81;
     for (int e = 0; e < 81; ++e) Sd[e] = Sm[e / 9][e % 9];
-    T *So = C.ws + C.L.So + (size_t)(1 + k) * 81;
+    T *So = C.So + (size_t)(1 + k) * 81;
     if (k + 1 < N) {
         const T *w1 = C.st(k + 1) + S::W;
         for (int i = 0; i < 9; ++i)
@@ -514,112 +602,110 @@ template <typename T, int ROBOT> __device__ void phase_sblock(const Ctx<T, ROBOT
     }
 }
 
-// (4) block Cholesky of S (wave 0).  Sd[j] <- Lc_j^-1 (lower), So[j] <- Lo_j = S_{j,j+1}' Lc_j^-T
+template <typename T> __device__ __forceinline__ T rcp_nr(T p) {
+    // reciprocal: hardware estimate + two Newton steps (full precision)
+    T r;
+    if constexpr (sizeof(T) == 8) r = __builtin_amdgcn_rcp(p); else r = __builtin_amdgcn_rcpf(p);
+    r = fma(r, fma(-p, r, T(1)), r);
+    r = fma(r, fma(-p, r, T(1)), r);
+    return r;
+}
+
+// (4) block-Thomas factorization of S with explicit symmetric inverses (wave 0, all 64 lanes):
+//   I_0 = S_00^-1;  X_j = S_{j-1,j}' I_{j-1};  I_j = (S_jj - X_j S_{j-1,j})^-1
+// Sd[j] <- I_j, So[j-1] <- X_j.  Inverses by Gauss-Jordan sweeps (SPD: no pivoting), with a
+// pivot floor (near the solution of a degenerate QP the last Schur blocks are differences of
+// O(M) numbers and may lose positivity by rounding).
 template <typename T> __device__ void seq_factor(T *Sd, T *So, int NB, T *sh) {
     const int lane = threadIdx.x & 63;
-    T *Lm = sh, *Li = sh + 81, *Lp = sh + 162;   // working block, its inverse, previous Lo
+    T *A = sh, *Xb = sh + 96;
+    const int e0 = lane, e1 = lane + 64;
+    const bool has1 = e1 < 81;
+    const int i0 = e0 / 9, c0 = e0 % 9, i1 = e1 / 9, c1 = e1 % 9;
     for (int j = 0; j < NB; ++j) {
-        const T *Sj = Sd + (size_t)j * 81;
-        for (int e = lane; e < 81; e += WAVE) {
-            const int i = e / 9, c = e % 9;
-            T v = Sj[e];
-            if (j > 0 && c <= i)
-                for (int m = 0; m < 9; ++m) v -= Lp[i * 9 + m] * Lp[c * 9 + m];
-            Lm[e] = v;
-        }
-        wave_sync();
-        // Cholesky (lower) in Lm, with a pivot floor (modified Cholesky): near the solution of
-        // a degenerate QP the last Schur blocks are differences of O(M) numbers
-        for (int c = 0; c < 9; ++c) {
-            const T d = sqrt(fmax(Lm[c * 9 + c], T(1e-13) * Sj[c * 9 + c]));
-            const T id = T(1) / d;
-            wave_sync();
-            if (lane > c && lane < 9) Lm[lane * 9 + c] *= id;
-            if (lane == c) Lm[c * 9 + c] = d;
-            wave_sync();
-            for (int e = lane; e < 81; e += WAVE) {
-                const int i = e / 9, q = e % 9;
-                if (q > c && i >= q) Lm[e] -= Lm[i * 9 + c] * Lm[q * 9 + c];
-            }
-            wave_sync();
-        }
-        // inverse of the lower factor, lane = column
-        if (lane < 9) {
-            const int c = lane;
-            for (int i = 0; i < 9; ++i) Li[i * 9 + c] = T(0);
-            Li[c * 9 + c] = T(1) / Lm[c * 9 + c];
-            for (int i = c + 1; i < 9; ++i) {
-                T v = T(0);
-                for (int q = c; q < i; ++q) v += Lm[i * 9 + q] * Li[q * 9 + c];
-                Li[i * 9 + c] = -v / Lm[i * 9 + i];
-            }
-        }
-        wave_sync();
         T *Dj = Sd + (size_t)j * 81;
-        for (int e = lane; e < 81; e += WAVE) Dj[e] = Li[e];
-        if (j + 1 < NB) {
-            const T *Oj = So + (size_t)j * 81;
-            T out[2];
-            for (int r = 0, e = lane; e < 81; e += WAVE, ++r) {   // Lo[i][c] = sum_m So[m][i] Li[c][m]
-                const int i = e / 9, c = e % 9;
-                T v = T(0);
-                for (int m = 0; m <= c; ++m) v += Oj[m * 9 + i] * Li[c * 9 + m];
-                out[r] = v;
+        if (j == 0) {
+            A[e0] = Dj[e0];
+            if (has1) A[e1] = Dj[e1];
+        } else {
+            const T *Ip = Sd + (size_t)(j - 1) * 81, *Op = So + (size_t)(j - 1) * 81;
+            T x0 = T(0), x1 = T(0);
+            for (int m = 0; m < 9; ++m) {
+                x0 = fma(Op[m * 9 + i0], Ip[m * 9 + c0], x0);
+                if (has1) x1 = fma(Op[m * 9 + i1], Ip[m * 9 + c1], x1);
+            }
+            Xb[e0] = x0;
+            if (has1) Xb[e1] = x1;
+            wave_sync();
+            T a0 = Dj[e0], a1 = has1 ? Dj[e1] : T(0);
+            for (int m = 0; m < 9; ++m) {
+                a0 = fma(-Xb[i0 * 9 + m], Op[m * 9 + c0], a0);
+                if (has1) a1 = fma(-Xb[i1 * 9 + m], Op[m * 9 + c1], a1);
             }
             wave_sync();
-            T *Oo = So + (size_t)j * 81;
-            for (int r = 0, e = lane; e < 81; e += WAVE, ++r) { Lp[e] = out[r]; Oo[e] = out[r]; }
+            A[e0] = a0;
+            T *Ow = So + (size_t)(j - 1) * 81;
+            Ow[e0] = x0;
+            if (has1) { A[e1] = a1; Ow[e1] = x1; }
         }
+        wave_sync();
+        for (int c = 0; c < 9; ++c) {
+            const T p = fmax(A[c * 9 + c], T(1e-13) * Dj[c * 9 + c]);
+            const T ip = rcp_nr(p);
+            const T aic0 = A[i0 * 9 + c], acj0 = A[c * 9 + c0], aij0 = A[e0];
+            T aic1 = T(0), acj1 = T(0), aij1 = T(0);
+            if (has1) { aic1 = A[i1 * 9 + c]; acj1 = A[c * 9 + c1]; aij1 = A[e1]; }
+            wave_sync();
+            auto upd = [&](int i, int cc, T aic, T acj, T aij) -> T {
+                if (i != c && cc != c) return fma(-aic * ip, acj, aij);
+                if (i == c && cc != c) return acj * ip;
+                if (i != c && cc == c) return -aic * ip;
+                return ip;
+            };
+            A[e0] = upd(i0, c0, aic0, acj0, aij0);
+            if (has1) A[e1] = upd(i1, c1, aic1, acj1, aij1);
+            wave_sync();
+        }
+        Dj[e0] = A[e0];
+        if (has1) Dj[e1] = A[e1];
         wave_sync();
     }
 }
 
-// (5c) forward / backward block sweeps: rhs -> dnu
-template <typename T> __device__ void seq_solve(const T *Li, const T *Lo, T *rhs, T *dnu, int NB, T *sh) {
+// (5c) forward / backward block sweeps with the Thomas factors: rhs -> dnu
+//   y_0 = b_0, y_j = b_j - X_j y_{j-1};  x_{NB-1} = I y;  x_j = I_j y_j - X_{j+1}' x_{j+1}
+// The right-hand side and the sweep vectors are staged in LDS (vb: NB*9 elements).
+template <typename T> __device__ void seq_solve(const T *Ii, const T *Xs, const T *rhs, T *dnu, int NB, T *vb) {
     const int lane = threadIdx.x & 63;
-    T *yp = sh, *tv = sh + 16;
-    if (lane < 9) yp[lane] = T(0);
+    for (int e = lane; e < NB * 9; e += WAVE) vb[e] = rhs[e];
     wave_sync();
-    for (int j = 0; j < NB; ++j) {
+    for (int j = 1; j < NB; ++j) {
         if (lane < 9) {
-            T v = rhs[(size_t)j * 9 + lane];
-            if (j > 0) {
-                const T *O = Lo + (size_t)(j - 1) * 81 + lane * 9;
-                for (int m = 0; m < 9; ++m) v -= O[m] * yp[m];
-            }
-            tv[lane] = v;
-        }
-        wave_sync();
-        if (lane < 9) {
-            const T *Lj = Li + (size_t)j * 81 + lane * 9;
-            T v = T(0);
-            for (int m = 0; m <= lane; ++m) v += Lj[m] * tv[m];
-            rhs[(size_t)j * 9 + lane] = v;
-            yp[lane] = v;
+            const T *X = Xs + (size_t)(j - 1) * 81 + lane * 9;
+            const T *yp = vb + (size_t)(j - 1) * 9;
+            T v = vb[(size_t)j * 9 + lane];
+            for (int m = 0; m < 9; ++m) v = fma(-X[m], yp[m], v);
+            vb[(size_t)j * 9 + lane] = v;
         }
         wave_sync();
     }
-    if (lane < 9) yp[lane] = T(0);
-    wave_sync();
     for (int j = NB - 1; j >= 0; --j) {
+        T v = T(0);
         if (lane < 9) {
-            T v = rhs[(size_t)j * 9 + lane];
+            const T *I = Ii + (size_t)j * 81 + lane * 9;   // symmetric: row == column
+            const T *y = vb + (size_t)j * 9;
+            for (int m = 0; m < 9; ++m) v = fma(I[m], y[m], v);
             if (j < NB - 1) {
-                const T *O = Lo + (size_t)j * 81;
-                for (int m = 0; m < 9; ++m) v -= O[m * 9 + lane] * yp[m];
+                const T *X = Xs + (size_t)j * 81;             // X_{j+1} stored at So[j]
+                const T *xn = vb + (size_t)(j + 1) * 9;
+                for (int m = 0; m < 9; ++m) v = fma(-X[m * 9 + lane], xn[m], v);
             }
-            tv[lane] = v;
         }
         wave_sync();
-        if (lane < 9) {
-            const T *Lj = Li + (size_t)j * 81;
-            T v = T(0);
-            for (int m = lane; m < 9; ++m) v += Lj[m * 9 + lane] * tv[m];
-            dnu[(size_t)j * 9 + lane] = v;
-            yp[lane] = v;
-        }
+        if (lane < 9) vb[(size_t)j * 9 + lane] = v;
         wave_sync();
     }
+    for (int e = lane; e < NB * 9; e += WAVE) dnu[e] = vb[e];
 }
 
 // r_hat = r_i - r_c / lambda for the rows of knot k  (rc supplied per mode)
@@ -643,24 +729,35 @@ template <typename T, int ROBOT> __device__ void phase_w(const Ctx<T, ROBOT> &C,
     constexpr int NI = R_::NI, NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
     const int N = C.N;
     const T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
-    T rh[NI], v[NI];
+    T rh[NI];
     rhat_rows(C, k, corr, sigma_mu, rh);
-    for (int r = 0; r < NI; ++r) v[r] = (r < R_::FR || r >= R_::CP) ? (lm[r] / s[r]) * rh[r] : T(0);
-    T gL[3], gt, gu[NU];
-    C.gtv(k, v, gL, gt, gu);
-    T vx[9], vu[NU];
+    const T *fx = C.ws + C.L.facx + (size_t)k * FX;
     const T *rdx = C.ws + C.L.rdx + (size_t)k * 9;
-    for (int i = 0; i < 9; ++i) vx[i] = rdx[i] + (i >= 6 ? gL[i - 6] : T(0));
-    const T vt = C.ws[C.L.rdt + k] + gt;
+    T *wx = C.ws + C.L.wx + (size_t)k * 9;
+    for (int i = 0; i < 6; ++i) wx[i] = fx[i] * rdx[i];
+    {   // (L, t): w = -(local solve with v = -r_d)
+        const T vL[3] = {-rdx[6], -rdx[7], -rdx[8]};
+        T dL[3], dt, dlt[8], dls;
+        tr_local(C, k, vL, -C.ws[C.L.rdt + k], rh, dL, dt, dlt, dls);
+        for (int i = 0; i < 3; ++i) wx[6 + i] = -dL[i];
+        C.ws[C.L.wt + k] = -dt;
+    }
+    T ou[NU];
     if (k < N) {
         const T *rdu = C.ws + C.L.rdu + (size_t)k * NU;
-        for (int i = 0; i < NU; ++i) vu[i] = rdu[i] + gu[i];
+        T vu[NU];
+        for (int i = 0; i < NU; ++i) vu[i] = rdu[i];
+        if (ROBOT == 1) {   // CoP rows (D-form, folded into W_cop)
+            for (int c = 0; c < NC; ++c) {
+                if (!C.logic[k * NC + c]) continue;
+                for (int dd = 0; dd < 2; ++dd) {
+                    const int r0 = R_::CP + 4 * c + 2 * dd;
+                    vu[NUPC * c + dd] += C.Dform(lm[r0], s[r0]) * rh[r0] - C.Dform(lm[r0 + 1], s[r0 + 1]) * rh[r0 + 1];
+                }
+            }
+        }
+        phi_solve_u(C, k, vu, ou);
     }
-    T ox[9], ot, ou[NU];
-    phi_solve(C, k, vx, vt, vu, ox, ot, ou);
-    T *wx = C.ws + C.L.wx + (size_t)k * 9;
-    for (int i = 0; i < 9; ++i) wx[i] = ox[i];
-    C.ws[C.L.wt + k] = ot;
     if (k < N) {
         for (int c = 0; c < NC; ++c) {
             if (!C.logic[k * NC + c]) continue;
@@ -719,22 +816,29 @@ __device__ T phase_dz(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu) {
     }
     if (k >= 1) for (int i = 0; i < 9; ++i) ex[i] -= dnu[(size_t)k * 9 + i];
     if (k == N) for (int i = 0; i < 9; ++i) ex[i] += dnu[(size_t)(N + 1) * 9 + i];
-    T ax[9], at, au[NU];
-    phi_solve(C, k, ex, T(0), eu, ax, at, au);
-    T dx[9], dtt, du[NU];
-    const T *wx = C.ws + C.L.wx + (size_t)k * 9, *wu = C.ws + C.L.wu + (size_t)k * NU;
-    for (int i = 0; i < 9; ++i) dx[i] = -wx[i] - ax[i];
-    dtt = -C.ws[C.L.wt + k] - at;
-    if (k < N) for (int i = 0; i < NU; ++i) du[i] = -wu[i] - au[i];
+    const T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
+    const T *rdi = C.ws + C.L.rdi + (size_t)k * NI;
+    T rh[NI];
+    rhat_rows(C, k, corr, sigma_mu, rh);
+    const T *fx = C.ws + C.L.facx + (size_t)k * FX;
+    const T *rdx = C.ws + C.L.rdx + (size_t)k * 9;
+    T dx[9], dtt, du[NU], dlt[8], dls;
+    for (int i = 0; i < 6; ++i) dx[i] = -fx[i] * (rdx[i] + ex[i]);
+    {
+        const T vL[3] = {-(rdx[6] + ex[6]), -(rdx[7] + ex[7]), -(rdx[8] + ex[8])};
+        tr_local(C, k, vL, -C.ws[C.L.rdt + k], rh, dx + 6, dtt, dlt, dls);
+    }
+    if (k < N) {
+        T au[NU];
+        phi_solve_u(C, k, eu, au);
+        const T *wu = C.ws + C.L.wu + (size_t)k * NU;
+        for (int i = 0; i < NU; ++i) du[i] = -wu[i] - au[i];
+    }
     T *gdx = C.ws + C.L.dx + (size_t)k * 9;
     for (int i = 0; i < 9; ++i) gdx[i] = dx[i];
     C.ws[C.L.dt + k] = dtt;
     if (k < N) { T *gdu = C.ws + C.L.du + (size_t)k * NU; for (int i = 0; i < NU; ++i) gdu[i] = du[i]; }
     // rows
-    const T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
-    const T *rdi = C.ws + C.L.rdi + (size_t)k * NI;
-    T rh[NI];
-    rhat_rows(C, k, corr, sigma_mu, rh);
     T *ds = C.ws + (corr ? C.L.ds : C.L.dsa) + (size_t)k * NI;
     T *dl = C.ws + (corr ? C.L.dl : C.L.dla) + (size_t)k * NI;
     T amax = T(1);
@@ -742,7 +846,9 @@ __device__ T phase_dz(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu) {
         if (!C.present(k, r)) { ds[r] = T(0); dl[r] = T(0); continue; }
         const T g = C.gz(k, r, dx, dtt, du, false);
         ds[r] = -rdi[r] - g;
-        if (r < R_::FR || r >= R_::CP) dl[r] = (lm[r] / s[r]) * (g + rh[r]);
+        if (r < 8) dl[r] = dlt[r];
+        else if (r == 8) dl[r] = dls;
+        else if (r >= R_::CP) dl[r] = C.Dform(lm[r], s[r]) * (g + rh[r]);
     }
     if (k < N) {
         // friction: dlam = Kinv (Gw v + rhat),  v = -(rdu + E'dnu_u) restricted to f
@@ -833,9 +939,10 @@ template <typename T, int ROBOT> __device__ void phase_init_shift(const Ctx<T, R
 }
 
 // ------------------------------------------------------------------ kernel
-template <typename T, int ROBOT>
+template <typename T, int ROBOT, bool SL>
 __global__ void __launch_bounds__(NT) k_qp_ipm(DevBuf<T> d, int only_active, int max_iter, T eps_abs, T eps_rel,
                                                T eta) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char dsmem[];
     constexpr int NI = Rows<ROBOT>::NI;
     const int b = blockIdx.x;
     if (b >= d.B) return;
@@ -843,14 +950,39 @@ __global__ void __launch_bounds__(NT) k_qp_ipm(DevBuf<T> d, int only_active, int
     __shared__ T red[8 * (NT / 64)];
     __shared__ T sh[256];
     const int tid = threadIdx.x, N = d.N, K1 = N + 1, NB = N + 2;
-    Ctx<T, ROBOT> C{N, nullptr, nullptr, nullptr, nullptr, T(0), T(0), nullptr, WsLayout(N, NI, Robot<ROBOT>::NC)};
+    Ctx<T, ROBOT> C{N, nullptr, nullptr, nullptr, nullptr, T(0), T(0), nullptr, WsLayout(N, NI, Robot<ROBOT>::NC),
+                    nullptr, nullptr, T(0)};
     C.prm = d.params + d.class_id[b];
     C.stage = d.stage + (size_t)b * K1 * Stage<ROBOT>::SIZE;
     C.logic = d.logic + (size_t)b * N * Robot<ROBOT>::NC;
     C.xbar = d.Xbar + (size_t)b * K1 * 9;
     C.cw = d.cw[b];
     C.beta = C.prm->dt / C.prm->mass;
+    {
+        T wmax = T(1);
+        for (int i = 0; i < 9; ++i) wmax = fmax(wmax, C.prm->Wx[i]);
+        C.dcap = T(1e12) * wmax;
+    }
     C.ws = d.ws + (size_t)b * d.ws_stride;
+    T *vbuf = reinterpret_cast<T *>(dsmem);
+    if (SL) {
+        C.Sd = vbuf + (((size_t)NB * 9 + 7) & ~size_t(7));
+        C.So = C.Sd + (size_t)NB * 81;
+    } else {
+        C.Sd = C.ws + C.L.Sd;
+        C.So = C.ws + C.L.So;
+    }
+#ifdef CMPC_STAMPS
+    unsigned long long t_prev = __builtin_amdgcn_s_memtime(), t_acc[12] = {};
+#define STAMP(i)                                                               \
+    do {                                                                       \
+        const unsigned long long t_now = __builtin_amdgcn_s_memtime();         \
+        t_acc[i] += t_now - t_prev;                                            \
+        t_prev = t_now;                                                        \
+    } while (0)
+#else
+#define STAMP(i) do { } while (0)
+#endif
     // ---- starting point of the initialization step: z = (xbar, ubar, 0), nu = 0, s = lambda = 1
     for (int k = tid; k < K1; k += NT) {
         T *x = C.var_x(k);
@@ -881,6 +1013,7 @@ __global__ void __launch_bounds__(NT) k_qp_ipm(DevBuf<T> d, int only_active, int
         block_reduce<T, NT, 6, 1>(mx, red);
         T sm2[2] = {nm.mu, nm.cnt};
         block_reduce<T, NT, 2, 0>(sm2, red);
+        STAMP(0);
         const T prim = mx[0], dual = mx[1], comp = mx[2], sp = mx[3], sdd = mx[4];
         const T mu = sm2[0] / fmax(sm2[1], T(1));
         const T ep = eps_abs + eps_rel * sp, ed = eps_abs + eps_rel * sdd;
@@ -897,9 +1030,12 @@ __global__ void __launch_bounds__(NT) k_qp_ipm(DevBuf<T> d, int only_active, int
         // ---- factorization
         for (int k = tid; k < K1; k += NT) phase_factor<T, ROBOT>(C, k);
         __syncthreads();
+        STAMP(1);
         for (int k = tid; k < K1; k += NT) phase_sblock<T, ROBOT>(C, k);
         __syncthreads();
-        if (tid < 64) seq_factor(C.ws + C.L.Sd, C.ws + C.L.So, NB, sh);
+        STAMP(2);
+        if (tid < 64) seq_factor(C.Sd, C.So, NB, sh);
+        STAMP(3);
         __syncthreads();
         // ---- predictor (affine) and corrector
         T sigma_mu = T(0);
@@ -907,13 +1043,17 @@ __global__ void __launch_bounds__(NT) k_qp_ipm(DevBuf<T> d, int only_active, int
         for (int corr = 0; corr < 2; ++corr) {
             for (int k = tid; k < K1; k += NT) phase_w<T, ROBOT>(C, k, corr, sigma_mu);
             __syncthreads();
+            STAMP(4);
             for (int k = tid; k < K1; k += NT) phase_rhs<T, ROBOT>(C, k);
             __syncthreads();
-            if (tid < 64) seq_solve(C.ws + C.L.Sd, C.ws + C.L.So, C.ws + C.L.rhs, C.ws + C.L.dnu, NB, sh);
+            STAMP(5);
+            if (tid < 64) seq_solve(C.Sd, C.So, C.ws + C.L.rhs, C.ws + C.L.dnu, NB, vbuf);
             __syncthreads();
+            STAMP(6);
             T am[1] = {T(1)};
             for (int k = tid; k < K1; k += NT) am[0] = fmin(am[0], phase_dz<T, ROBOT>(C, k, corr, sigma_mu));
             block_reduce<T, NT, 1, 2>(am, red);
+            STAMP(7);
             alpha = am[0];
             if (init) break;
             if (corr == 0) {
@@ -938,6 +1078,7 @@ __global__ void __launch_bounds__(NT) k_qp_ipm(DevBuf<T> d, int only_active, int
         alpha = fmin(T(1), eta * alpha);
         for (int k = tid; k < K1; k += NT) phase_update<T, ROBOT>(C, k, alpha);
         __syncthreads();
+        STAMP(8);
     }
     // ---- outputs: solution and multipliers
     for (int k = tid; k < K1; k += NT) {
@@ -952,15 +1093,24 @@ __global__ void __launch_bounds__(NT) k_qp_ipm(DevBuf<T> d, int only_active, int
     if (tid == 0) {
         d.qp_status[b] = status;
         d.qp_iters[b] = it;
+#ifdef CMPC_STAMPS
+        for (int i = 0; i < 12; ++i) d.stamps[(size_t)b * 16 + i] = t_acc[i];
+#endif
     }
+#undef STAMP
 }
 
-#define INST(T, R) template __global__ void k_qp_ipm<T, R>(DevBuf<T>, int, int, T, T, T);
+#define INST(T, R)                                                                   \
+    template __global__ void k_qp_ipm<T, R, false>(DevBuf<T>, int, int, T, T, T);     \
+    template __global__ void k_qp_ipm<T, R, true>(DevBuf<T>, int, int, T, T, T);
 INST(double, 0)
 INST(double, 1)
 INST(float, 0)
 INST(float, 1)
 #undef INST
+
+size_t ipm_vec_lds_bytes(int N, int prec_bytes) { return (((size_t)(N + 2) * 9 + 7) & ~size_t(7)) * prec_bytes; }
+size_t ipm_schur_lds_bytes(int N, int prec_bytes) { return (size_t)(2 * N + 3) * 81 * prec_bytes; }
 
 size_t ipm_workspace_elems(int N, int robot) {
     return robot == 0 ? WsLayout(N, Rows<0>::NI, Robot<0>::NC).total : WsLayout(N, Rows<1>::NI, Robot<1>::NC).total;

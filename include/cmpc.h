@@ -80,8 +80,8 @@ typedef struct {
 /* QP solver settings (defaults by cmpc_default_qp_settings) */
 typedef struct {
     int32_t max_iter;       /* interior-point iterations (default 60) */
-    double eps_abs;         /* absolute tolerance (fp64 default 1e-10, fp32 1e-6) */
-    double eps_rel;         /* relative tolerance (fp64 default 1e-10, fp32 1e-6) */
+    double eps_abs;         /* absolute tolerance (fp64 default 1e-11, fp32 1e-6) */
+    double eps_rel;         /* relative tolerance (fp64 default 1e-11, fp32 1e-6) */
     double step_fraction;   /* fraction-to-boundary (default 0.99) */
 } cmpc_qp_settings;
 
@@ -137,6 +137,9 @@ int cmpc_timing_begin(cmpc_handle h);
 int cmpc_timing_end(cmpc_handle h, cmpc_timing *t, int *n_iterations);
 /* Sum over problems of the interior-point iterations of the last QP solve. */
 int cmpc_get_qp_iterations_total(cmpc_handle h, int64_t *total);
+/* Diagnostic builds (libcmpc_diag.so, -DCMPC_STAMPS): per-problem shader-cycle counters of the
+ * QP kernel's phases, (B, 16); zeros in the production library. */
+int cmpc_debug_stamps(cmpc_handle h, uint64_t *out);
 
 #ifdef __cplusplus
 }

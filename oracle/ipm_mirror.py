@@ -62,7 +62,7 @@ def _fslot(qp):
     return 0 if qp.robot == 'solo12' else 2
 
 
-def solve(qp, eps=1e-10, max_iter=60, eta=0.99, verbose=False, reg=0.0, piv_floor=1e-13):
+def solve(qp, eps=1e-11, max_iter=60, eta=0.99, verbose=False, reg=0.0, piv_floor=1e-13, dcap_rel=1e12):
     N, nc, nu, nupc = qp.N, qp.nc, qp.nu, qp.nupc
     fo = _fslot(qp)
     talos = qp.robot != 'solo12'
@@ -173,13 +173,32 @@ def solve(qp, eps=1e-10, max_iter=60, eta=0.99, verbose=False, reg=0.0, piv_floo
             break
         # ---- factorization ----
         D = [li / si * mk for li, si, mk in zip(lam, s, masks)]
+        # cap D on the rows handled in D-form (TR, slack, CoP): beyond ~1e12 x the stage
+        # curvature the products D * r lose all precision; the capped Newton step is an inexact
+        # Newton step on exact residuals (convergence is driven by the residuals)
+        dcap = dcap_rel * max(float(np.max(qp.Wx)), 1.0)
+        if talos:
+            D[3] = np.minimum(D[3], dcap)
         # x/t block: Phi_LL, Phi_Lt, Phi_tt
-        PhiLL = np.zeros((N + 1, 3, 3)) + np.diag(qp.Wx[6:9])[None]
-        PhiLL += np.einsum('kj,ja,jb->kab', D[0], PENUM, PENUM)
-        PhiLt = qp.cw * (D[0] @ PENUM)
-        Phitt = qp.cw ** 2 * D[0].sum(axis=1) + D[1]
-        MLLinv = PhiLL - np.einsum('ka,kb->kab', PhiLt, PhiLt) / Phitt[:, None, None]
-        ML = np.linalg.inv(MLLinv)                       # (N+1,3,3)
+        # (L, t) block in push-through form.  Unknowns dL (3), dt, dlam_TR (8), dlam_sl:
+        #   W dL + G' dlam = vL ;  cw 1'dlam - dlam_sl = vt ;  G dL + cw 1 dt - D^-1 dlam = -rh ;
+        #   -dt - D_sl^-1 dlam_sl = -rh_sl
+        # eliminated with K = D_TR^-1 + G W^-1 G' (8x8 SPD, floored), k = K^-1 1, kap = 1'k:
+        #   dt = (vt + D_sl rh_sl - cw 1'K^-1 a) / (D_sl + cw^2 kap),  a = G W^-1 vL + rh
+        #   dlam = K^-1 a + cw dt k ;  dL = W^-1 (vL - G'dlam) ;  dlam_sl = cw 1'dlam - vt
+        WLi = 1.0 / qp.Wx[6:9]
+        YL = PENUM * WLi[None, :]                                  # G W^-1 (8x3)
+        GWG_tr = PENUM @ YL.T                                       # (8x8)
+        DinvT = np.where(D[0] > 0, 1.0 / np.maximum(D[0], 1e-300), 1e300)
+        kfl = 1e-12 * np.trace(GWG_tr)
+        Ktr = GWG_tr[None] + np.maximum(DinvT, kfl)[:, :, None] * np.eye(8)[None]
+        Ktr_inv = np.linalg.inv(Ktr)                                # (N+1,8,8)
+        kvec = Ktr_inv.sum(axis=2)                                  # K^-1 1
+        kap = kvec.sum(axis=1)
+        Dsl = D[1]
+        den = Dsl + qp.cw ** 2 * kap
+        Pm = Ktr_inv - qp.cw ** 2 * np.einsum('ka,kb->kab', kvec, kvec) / den[:, None, None]
+        ML = np.diag(WLi)[None] - np.einsum('ja,kjl,lb->kab', YL, Pm, YL)
         Mfull = np.zeros((N + 1, 9, 9))
         Mfull[:, np.arange(6), np.arange(6)] = 1.0 / qp.Wx[:6]
         Mfull[:, 6:9, 6:9] = ML
@@ -195,7 +214,10 @@ def solve(qp, eps=1e-10, max_iter=60, eta=0.99, verbose=False, reg=0.0, piv_floo
                 Winv[:, :, d, d] = 1.0 / (Wu_b[None, :, d] + dcop[:, :, d])
         Gw = np.einsum('kirm,kimn->kirn', qp.G, Winv[:, :, fo:fo + 3, fo:fo + 3])    # G W^-1 (N,nc,4,3)
         Dinv_f = np.where(fm > 0, s[2] / np.where(fm > 0, lam[2], 1.0), 1.0)
-        Kf = np.einsum('kirn,kiqn->kirq', Gw, qp.G) + Dinv_f[..., None] * np.eye(4)
+        GWG = np.einsum('kirn,kiqn->kirq', Gw, qp.G)
+        # floor on D^-1: at a zero force all four pyramid rows are active (degenerate, K -> rank 3)
+        kfloor = 1e-12 * np.trace(GWG, axis1=2, axis2=3)[..., None] + 1e-300
+        Kf = GWG + np.maximum(Dinv_f, kfloor)[..., None] * np.eye(4)
         Kf = np.where(fm[..., None] > 0, Kf, np.eye(4))                 # inactive contacts: identity
         Gw = Gw * fm[..., None]
         Kf_inv = np.linalg.inv(Kf)
@@ -224,28 +246,48 @@ def solve(qp, eps=1e-10, max_iter=60, eta=0.99, verbose=False, reg=0.0, piv_floo
                 Lo[j] = np.linalg.solve(Lc[j], So[j]).T        # (S_{j,j+1})^T Lc^-T
                 Sh = Sd[j + 1] - Lo[j] @ Lo[j].T
 
+        def tr_local(vL, vt, rh_tr, rh_sl):
+            """(dL, dt, dlam_TR, dlam_sl) of the (L, t) block (see the factorization)."""
+            a = vL @ YL.T + rh_tr                                   # (N+1, 8)
+            ka = np.einsum('kab,kb->ka', Ktr_inv, a)
+            dt_ = (vt + Dsl * rh_sl - qp.cw * ka.sum(axis=1)) / den
+            dlt = ka + qp.cw * dt_[:, None] * kvec
+            dL = WLi[None, :] * (vL - dlt @ PENUM)
+            dls = qp.cw * dlt.sum(axis=1) - vt
+            return dL, dt_, dlt, dls
+
+        def u_local(vu, rh_f, rh_cp):
+            """(du, dlam_fric) of the control blocks: friction rows in push-through form, CoP
+            rows folded into the diagonal."""
+            vu = vu.reshape(N, nc, nupc).copy()
+            if talos:
+                vu[:, :, 0:2] += -(D[3][..., 0] * rh_cp[..., 0] - D[3][..., 1] * rh_cp[..., 1])
+            du_ = np.einsum('kiab,kib->kia', Winv, vu)
+            vf = vu[:, :, fo:fo + 3]
+            z = np.einsum('kirn,kin->kir', Gw, vf) + rh_f
+            dlf = np.einsum('kirq,kiq->kir', Kf_inv, z) * fm
+            gl = np.einsum('kirm,kir->kim', qp.G, dlf)
+            du_[:, :, fo:fo + 3] = np.einsum('kiab,kib->kia', Winv[:, :, fo:fo + 3, fo:fo + 3], vf - gl)
+            return du_.reshape(N, nu), dlf
+
         def phi_solve(vx, vt, vu):
-            """Phi^-1 (vx, vt, vu) with t eliminated per knot."""
-            vx = vx.copy()
-            vx[:, 6:9] -= PhiLt * (vt / Phitt)[:, None]
-            dx = np.einsum('kij,kj->ki', Mfull, vx)
-            dt_ = (vt - np.einsum('ka,ka->k', PhiLt, dx[:, 6:9])) / Phitt
-            du = np.einsum('kiab,kib->kia', Phiuinv, vu.reshape(N, nc, nupc)).reshape(N, nu)
-            return dx, dt_, du
+            """Phi^-1 (vx, vt, vu) (no row terms)."""
+            dx = vx / qp.Wx[None, :]
+            dL, dt_, _, _ = tr_local(vx[:, 6:9], vt, np.zeros((N + 1, 8)), np.zeros(N + 1))
+            dx[:, 6:9] = dL
+            du_, _ = u_local(vu, np.zeros((N, nc, 4)), np.zeros((N, nc, 2, 2)) if talos else None)
+            return dx, dt_, du_
 
         def newton(rc):
-            # rhat_i = r_i - r_c / lambda ; x/t rows use the Phi form, friction rows the stable form
             rhat = [(ri - c / np.where(mk > 0, li, 1.0)) * mk for ri, c, li, mk in zip(rdi, rc, lam, masks)]
-            w = [d * rh for d, rh in zip(D, rhat)]
-            w[2] = np.zeros_like(w[2])
-            gx_, gt_, gu_ = GT(w)
-            vx, vt, vu = rdx + gx_, rdt + gt_, rdu + gu_
-            wx, wt, wu = phi_solve(vx, vt, vu)
-            # friction particular part: W^-1 G' K^-1 rhat_fric
-            kr = np.einsum('kirq,kiq->kir', Kf_inv, rhat[2])
-            wu_f = np.zeros((N, nc, nupc))
-            wu_f[:, :, fo:fo + 3] = np.einsum('kirn,kir->kin', Gw, kr)
-            wu = wu + wu_f.reshape(N, nu)
+            rcp = rhat[3] if talos else None
+            # particular solution w = Phi^-1 (r_d + G'D rhat): local solves with v = -r_d
+            wx = rdx / qp.Wx[None, :]
+            dL, dt0, _, _ = tr_local(-rdx[:, 6:9], -rdt, rhat[0], rhat[1])
+            wx[:, 6:9] = -dL
+            wt = -dt0
+            du0, _ = u_local(-rdu, rhat[2], rcp)
+            wu = -du0
             rhs = rde - Ez(wx, wu)
             # forward / backward block substitution
             y = np.zeros((N + 2, 9))
@@ -257,16 +299,16 @@ def solve(qp, eps=1e-10, max_iter=60, eta=0.99, verbose=False, reg=0.0, piv_floo
                 b = y[j] - (Lo[j].T @ dnu[j + 1] if j < N + 1 else 0)
                 dnu[j] = np.linalg.solve(Lc[j].T, b)
             ex_, eu_ = ET(dnu)
-            ax, at, au = phi_solve(ex_, np.zeros(N + 1), eu_)
-            dx = -wx - ax; dt_ = -wt - at; du = -wu - au
+            # full direction from the local solves with v = -(r_d + E'dnu)
+            vx = -(rdx + ex_); vu = -(rdu + eu_)
+            dx = vx / qp.Wx[None, :]
+            dL, dt_, dlt, dls = tr_local(vx[:, 6:9], -rdt, rhat[0], rhat[1])
+            dx[:, 6:9] = dL
+            du, dlf = u_local(vu, rhat[2], rcp)
             gz = Gz(dx, du, dt_)
-            dl = [(d * (g + rh)) * mk for d, g, rh, mk in zip(D, gz, rhat, masks)]
-            # friction: dlam = K^-1 (G W^-1 v + rhat), v = -(r_d,u + (E'dnu)_u)  (no D * r products)
-            vfull = -(rdu + eu_)
+            dl = [dlt, dls, dlf]
             if talos:
-                vtmp = vfull.reshape(N, nc, nupc).copy()
-            vf = vfull.reshape(N, nc, nupc)[:, :, fo:fo + 3]
-            dl[2] = np.einsum('kirq,kiq->kir', Kf_inv, np.einsum('kirn,kin->kir', Gw, vf) + rhat[2]) * fm
+                dl.append(D[3] * (gz[3] + rhat[3]) * masks[3])
             ds = [(-ri - g) * mk for ri, g, mk in zip(rdi, gz, masks)]
             return dx, dt_, du, dnu, dl, ds
 

@@ -1,0 +1,22 @@
+"""Per-phase cycle shares of the QP kernel (diagnostic library, CMPC_LIB_VARIANT=diag)."""
+import os, sys, time
+os.environ['CMPC_LIB_VARIANT'] = 'diag'
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, 'centroidal-mpc_amd')]
+import numpy as np
+from cmpc._lib import Solver
+from cmpc.synth import make_batch
+cfg = sys.argv[1] if len(sys.argv) > 1 else 'trot'
+N = int(sys.argv[2]) if len(sys.argv) > 2 else 100
+B = int(sys.argv[3]) if len(sys.argv) > 3 else 256
+pb = make_batch(cfg, N, B)
+s = Solver(pb.robot, N, B, 'fp64'); s.upload(pb)
+s.scp_iterate(True); s.synchronize()
+s.timing_begin(); s.scp_iterate(True); t = s.timing_end()
+st = s.debug_stamps().astype(float)
+names = ['residual', 'factor', 'sblock', 'seq_factor', 'phase_w', 'rhs', 'seq_solve', 'dz', 'update']
+its = s.qp_iterations_total() / B
+tot = st[:, :9].sum(axis=1).mean()
+print('B', B, 'N', N, 'qp_ms', t['qp_ms'], 'ipm iters', its, 'cycles/problem %.3g' % tot)
+for i, n in enumerate(names):
+    print('  %-11s %5.1f%%  %.3g cycles/IPM-iter' % (n, 100 * st[:, i].mean() / tot, st[:, i].mean() / its))
