@@ -46,7 +46,8 @@ class Timing(ctypes.Structure):
 
 
 EXPORTS = ['cmpc_create', 'cmpc_destroy', 'cmpc_last_error', 'cmpc_version', 'cmpc_default_qp_settings',
-           'cmpc_set_qp_settings', 'cmpc_set_params', 'cmpc_upload', 'cmpc_linearize', 'cmpc_assemble',
+           'cmpc_set_qp_settings', 'cmpc_set_params', 'cmpc_upload', 'cmpc_set_trust_region', 'cmpc_rollout',
+           'cmpc_linearize', 'cmpc_assemble',
            'cmpc_qp_solve', 'cmpc_accept', 'cmpc_scp_iterate', 'cmpc_solve_scp', 'cmpc_synchronize',
            'cmpc_get_linearization', 'cmpc_qp_sizes', 'cmpc_export_qp', 'cmpc_get_qp_solution',
            'cmpc_get_solution', 'cmpc_get_iteration_log', 'cmpc_get_timing', 'cmpc_timing_begin',
@@ -77,6 +78,8 @@ def load():
         'cmpc_set_qp_settings': (i32, [h, P(QPSettings)]),
         'cmpc_set_params': (i32, [h, i32, P(Params)]),
         'cmpc_upload': (i32, [h, i32, vp, vp, vp, vp, vp, vp]),
+        'cmpc_set_trust_region': (i32, [h, vp, vp]),
+        'cmpc_rollout': (i32, [h, vp, vp, vp]),
         'cmpc_linearize': (i32, [h]),
         'cmpc_assemble': (i32, [h]),
         'cmpc_qp_solve': (i32, [h]),
@@ -204,6 +207,23 @@ class Solver:
         self.B = pb.B
 
     # ---- phases
+    def set_trust_region(self, weight=None, radius=None):
+        """Per-problem trust-region weight / radius (scalars broadcast to the batch)."""
+        def arr(v):
+            return None if v is None else np.ascontiguousarray(np.broadcast_to(np.asarray(v, float), (self.B,)))
+        w, r = arr(weight), arr(radius)
+        self._chk(self.lib.cmpc_set_trust_region(self.h, _ptr(w), _ptr(r)), 'cmpc_set_trust_region')
+
+    def rollout(self, X, U):
+        """Nonlinear rollout along X (B, N+1, 9), U (B, N, nu) -> (B, N+1, 9) on the device."""
+        X = np.ascontiguousarray(X, dtype=float)
+        U = np.ascontiguousarray(U, dtype=float)
+        if X.shape != (self.B, self.N + 1, 9) or U.shape != (self.B, self.N, self.nu):
+            raise ValueError('rollout expects X %s and U %s' % ((self.B, self.N + 1, 9), (self.B, self.N, self.nu)))
+        out = np.zeros_like(X)
+        self._chk(self.lib.cmpc_rollout(self.h, _ptr(X), _ptr(U), _ptr(out)), 'cmpc_rollout')
+        return out
+
     def linearize(self): self._chk(self.lib.cmpc_linearize(self.h), 'cmpc_linearize')
     def assemble(self): self._chk(self.lib.cmpc_assemble(self.h), 'cmpc_assemble')
     def qp_solve(self): self._chk(self.lib.cmpc_qp_solve(self.h), 'cmpc_qp_solve')

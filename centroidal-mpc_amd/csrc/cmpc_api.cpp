@@ -21,6 +21,7 @@ template <typename T, int R, bool SL> __global__ void k_qp_ipm(DevBuf<T>, int, i
 size_t ipm_schur_lds_bytes(int N, int prec_bytes);
 size_t ipm_vec_lds_bytes(int N, int prec_bytes);
 template <typename T, int R> __global__ void k_accept(DevBuf<T>, int);
+template <typename T, int R> __global__ void k_rollout(DevBuf<T>, const T *, const T *, T *);
 size_t ipm_workspace_elems(int N, int robot);
 }  // namespace cmpc
 
@@ -231,6 +232,26 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
     HIPCHK(hipGetLastError());
 }
 
+template <typename T, int R> void rollout_impl(cmpc_handle h, const double *X, const double *U, double *out) {
+    const size_t nx = (size_t)h->B * (h->N + 1) * 9, nu = (size_t)h->B * h->N * NU;
+    void *dX = nullptr, *dU = nullptr, *dO = nullptr;
+    HIPCHK(hipMalloc(&dX, nx * sizeof(T)));
+    HIPCHK(hipMalloc(&dU, nu * sizeof(T)));
+    HIPCHK(hipMalloc(&dO, nx * sizeof(T)));
+    struct Free {
+        void *p[3];
+        ~Free() { for (void *q : p) if (q) (void)hipFree(q); }
+    } fr{{dX, dU, dO}};
+    to_dev<T>(h, dX, X, nx);
+    // U arrives with the handle's per-knot width NU (zero-padded contacts beyond nu)
+    to_dev<T>(h, dU, U, nu);
+    const long n = (long)h->B * (h->N + 1);
+    hipLaunchKernelGGL((k_rollout<T, R>), dim3((unsigned)((n + 127) / 128)), dim3(128), 0, h->stream, h->buf<T>(),
+                       (const T *)dX, (const T *)dU, (T *)dO);
+    HIPCHK(hipGetLastError());
+    from_dev<T>(h, out, dO, nx);
+}
+
 void phase(cmpc_handle h, int ph, int only_active) {
     need(h->B > 0, "no problems uploaded");
     need(h->n_classes > 0, "parameters not set");
@@ -415,6 +436,32 @@ int cmpc_upload(cmpc_handle h, int B, const int32_t *class_id, const int8_t *log
         up(h->Xbar, Xbar, (size_t)B * (N + 1) * 9);
         up(h->Ubar, Ubar, (size_t)B * N * NU);
         reset_scp(h, class_id);
+    });
+}
+
+int cmpc_set_trust_region(cmpc_handle h, const double *weight, const double *radius) {
+    return guard(h, [&] {
+        need(h->B > 0, "no problems uploaded");
+        auto st = get_scp(h);
+        for (int b = 0; b < h->B; ++b) {
+            if (weight) { need(weight[b] > 0, "trust-region weight must be > 0"); st[b].weight = weight[b]; }
+            if (radius) { need(radius[b] > 0, "trust-region radius must be > 0"); st[b].radius = radius[b]; }
+        }
+        HIPCHK(hipMemcpyAsync(h->scp, st.data(), st.size() * sizeof(ScpState), hipMemcpyHostToDevice, h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+    });
+}
+
+int cmpc_rollout(cmpc_handle h, const double *X, const double *U, double *out) {
+    return guard(h, [&] {
+        need(h->B > 0, "no problems uploaded");
+        need(h->n_classes > 0, "parameters not set");
+        need(X && U && out, "null buffer");
+        if (h->prec == CMPC_PREC_F64) {
+            if (h->robot == 0) rollout_impl<double, 0>(h, X, U, out); else rollout_impl<double, 1>(h, X, U, out);
+        } else {
+            if (h->robot == 0) rollout_impl<float, 0>(h, X, U, out); else rollout_impl<float, 1>(h, X, U, out);
+        }
     });
 }
 

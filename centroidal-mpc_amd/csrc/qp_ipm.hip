@@ -22,8 +22,8 @@ namespace cmpc {
 
 constexpr int NT = 256;
 constexpr int FU = 34;   // per-contact factor record: Gw 12 | Kinv 10 | F 6 | Winvd 6
-// per-knot (x, t) factor record: 1/Wx[0:6] | M_LL packed 6 | chol(K_TR) packed 36 | z1 = L^-1 1 (8) |
-// den | D_slack  (K_TR = D_TR^-1 + G_L W_L^-1 G_L', see phase_factor)
+// per-knot (x, t) factor record: 1/Wx[0:6] | M_LL packed 6 | chol(K_TR) packed 36 (diagonal as 1/L_jj) | z1 = L^-1 1 (8) |
+// 1/den | D_slack  (K_TR = D_TR^-1 + G_L W_L^-1 G_L', see phase_factor)
 constexpr int FX = 64, FX_ML = 6, FX_L = 12, FX_Z1 = 48, FX_DEN = 56, FX_DSL = 57;
 
 // Workspace offsets (elements) for one problem.
@@ -43,6 +43,21 @@ struct WsLayout {
         total = o;
     }
 };
+
+template <typename T> __device__ __forceinline__ T rcp_nr(T p) {
+    // reciprocal: hardware estimate + two Newton steps (full precision)
+    T r;
+    if constexpr (sizeof(T) == 8) r = __builtin_amdgcn_rcp(p); else r = __builtin_amdgcn_rcpf(p);
+    r = fma(r, fma(-p, r, T(1)), r);
+    r = fma(r, fma(-p, r, T(1)), r);
+    return r;
+}
+// LDS-qualified element type (keeps ds_* instructions in outlined helpers)
+template <typename T> using LdsT = __attribute__((address_space(3))) T;
+
+// a / b as a * (1 / b): the IEEE fp64 division is a ~10-instruction sequence; the reciprocal with
+// two Newton steps is within an ulp or two, which the interior-point iteration does not notice
+template <typename T> __device__ __forceinline__ T fdiv(T a, T b) { return a * rcp_nr(b); }
 
 template <typename T> __device__ __forceinline__ T tr_sign(int j, int i) { return ((j >> i) & 1) ? T(-1) : T(1); }
 
@@ -117,7 +132,7 @@ template <typename T, int ROBOT> struct Ctx {
     WsLayout L;
     T *Sd, *So;           // Schur blocks: LDS-resident when they fit (SL), else workspace
     T dcap;               // cap on D = lambda/s for the CoP rows (D-form, folded into W_cop)
-    __device__ T Dform(T l, T s_) const { return fmin(l / s_, dcap); }
+    __device__ T Dform(T l, T s_) const { return fmin(fdiv(l, s_), dcap); }
 
     __device__ const T *st(int k) const { return stage + (size_t)k * S::SIZE; }
     __device__ bool present(int k, int row) const {
@@ -204,16 +219,16 @@ template <typename T> __device__ void inv4spd(T (&a)[4][4], T *out) {
         for (int i = j + 1; i < 4; ++i) {
             T v = a[i][j];
             for (int q = 0; q < j; ++q) v -= Lm[i][q] * Lm[j][q];
-            Lm[i][j] = v / d;
+            Lm[i][j] = fdiv(v, d);
         }
     }
     T Li[4][4] = {};
+    for (int c = 0; c < 4; ++c) Li[c][c] = rcp_nr(Lm[c][c]);
     for (int c = 0; c < 4; ++c) {
-        Li[c][c] = T(1) / Lm[c][c];
         for (int i = c + 1; i < 4; ++i) {
             T v = T(0);
             for (int q = c; q < i; ++q) v += Lm[i][q] * Li[q][c];
-            Li[i][c] = -v / Lm[i][i];
+            Li[i][c] = -v * Li[i][i];
         }
     }
     int p = 0;
@@ -237,8 +252,8 @@ template <typename T> __device__ void chol8(T (&a)[36]) {
         T d = d0;
         for (int q = 0; q < j; ++q) d -= a[j * (j + 1) / 2 + q] * a[j * (j + 1) / 2 + q];
         d = sqrt(fmax(d, T(KFLOOR<T>) * d0));
-        a[j * (j + 1) / 2 + j] = d;
-        const T id = T(1) / d;
+        const T id = rcp_nr(d);
+        a[j * (j + 1) / 2 + j] = id;   // the factor record keeps 1 / L_jj
         for (int i = j + 1; i < 8; ++i) {
             T v = a[i * (i + 1) / 2 + j];
             for (int q = 0; q < j; ++q) v -= a[i * (i + 1) / 2 + q] * a[j * (j + 1) / 2 + q];
@@ -359,7 +374,7 @@ template <typename T, int ROBOT> __device__ void phase_factor(const Ctx<T, ROBOT
         for (int q = 0; q <= j; ++q) {
             T v = T(0);
             for (int i = 0; i < 3; ++i) v += tr_sign<T>(j, i) * tr_sign<T>(q, i) * wl[i];
-            if (q == j) v += fmax(s[j] / lm[j], kfl);
+            if (q == j) v += fmax(fdiv(s[j], lm[j]), kfl);
             Lk[j * (j + 1) / 2 + q] = v;
         }
     chol8(Lk);
@@ -372,7 +387,7 @@ template <typename T, int ROBOT> __device__ void phase_factor(const Ctx<T, ROBOT
             a1 -= l * z1[q];
             for (int i = 0; i < 3; ++i) az[i] -= l * Z[q][i];
         }
-        const T il = T(1) / Lk[j * (j + 1) / 2 + j];
+        const T il = Lk[j * (j + 1) / 2 + j];
         z1[j] = a1 * il;
         for (int i = 0; i < 3; ++i) Z[j][i] = az[i] * il;
     }
@@ -381,18 +396,18 @@ template <typename T, int ROBOT> __device__ void phase_factor(const Ctx<T, ROBOT
         kap += z1[j] * z1[j];
         for (int i = 0; i < 3; ++i) g[i] += Z[j][i] * z1[j];
     }
-    const T dsl = lm[8] / s[8];
-    const T den = dsl + C.cw * C.cw * kap;
+    const T dsl = fdiv(lm[8], s[8]);
+    const T iden = rcp_nr(dsl + C.cw * C.cw * kap);
     for (int i = 0; i < 6; ++i) fx[i] = T(1) / P.Wx[i];
     for (int i = 0, p = 0; i < 3; ++i)
         for (int q = 0; q <= i; ++q, ++p) {
             T zz = T(0);
             for (int j = 0; j < 8; ++j) zz += Z[j][i] * Z[j][q];
-            fx[FX_ML + p] = (i == q ? wl[i] : T(0)) - zz + C.cw * C.cw * g[i] * g[q] / den;
+            fx[FX_ML + p] = (i == q ? wl[i] : T(0)) - zz + C.cw * C.cw * g[i] * g[q] * iden;
         }
     for (int e = 0; e < 36; ++e) fx[FX_L + e] = Lk[e];
     for (int j = 0; j < 8; ++j) fx[FX_Z1 + j] = z1[j];
-    fx[FX_DEN] = den;
+    fx[FX_DEN] = iden;
     fx[FX_DSL] = dsl;
     if (k >= N) return;
     for (int c = 0; c < NC; ++c) {
@@ -428,7 +443,7 @@ template <typename T, int ROBOT> __device__ void phase_factor(const Ctx<T, ROBOT
         for (int r = 0; r < 4; ++r) tr += Km[r][r];
         // floor on D^-1: at a zero force all four pyramid rows are active (K -> rank 3)
         const T kfloor = T(KFLOOR<T>) * tr + T(sizeof(T) == 8 ? 1e-300 : 1e-37);
-        for (int r = 0; r < 4; ++r) Km[r][r] += fmax(s[R_::FR + 4 * c + r] / lm[R_::FR + 4 * c + r], kfloor);
+        for (int r = 0; r < 4; ++r) Km[r][r] += fmax(fdiv(s[R_::FR + 4 * c + r], lm[R_::FR + 4 * c + r]), kfloor);
         T Ki[10];
         inv4spd(Km, Ki);
         for (int q = 0; q < 10; ++q) fu[12 + q] = Ki[q];
@@ -466,22 +481,22 @@ template <typename T, int ROBOT>
 __device__ void tr_local(const Ctx<T, ROBOT> &C, int k, const T *vL, T vt, const T *rh, T *dL, T &dt, T *dlt, T &dls) {
     const T *fx = C.ws + C.L.facx + (size_t)k * FX;
     const T *Lk = fx + FX_L, *z1 = fx + FX_Z1;
-    const T wl[3] = {T(1) / C.prm->Wx[6], T(1) / C.prm->Wx[7], T(1) / C.prm->Wx[8]};
+    const T wl[3] = {rcp_nr(C.prm->Wx[6]), rcp_nr(C.prm->Wx[7]), rcp_nr(C.prm->Wx[8])};
     T y[8];
     for (int j = 0; j < 8; ++j) {
         T v = rh[j];
         for (int i = 0; i < 3; ++i) v += tr_sign<T>(j, i) * wl[i] * vL[i];
         for (int q = 0; q < j; ++q) v -= Lk[j * (j + 1) / 2 + q] * y[q];
-        y[j] = v / Lk[j * (j + 1) / 2 + j];
+        y[j] = v * Lk[j * (j + 1) / 2 + j];
     }
     T zy = T(0);
     for (int j = 0; j < 8; ++j) zy += z1[j] * y[j];
-    dt = (vt + fx[FX_DSL] * rh[8] - C.cw * zy) / fx[FX_DEN];
+    dt = (vt + fx[FX_DSL] * rh[8] - C.cw * zy) * fx[FX_DEN];
     for (int j = 0; j < 8; ++j) y[j] += C.cw * dt * z1[j];
     for (int j = 7; j >= 0; --j) {
         T v = y[j];
         for (int q = j + 1; q < 8; ++q) v -= Lk[q * (q + 1) / 2 + j] * dlt[q];
-        dlt[j] = v / Lk[j * (j + 1) / 2 + j];
+        dlt[j] = v * Lk[j * (j + 1) / 2 + j];
     }
     T sl = T(0);
     for (int j = 0; j < 8; ++j) sl += dlt[j];
@@ -602,110 +617,181 @@ template <typename T, int ROBOT> __device__ void phase_sblock(const Ctx<T, ROBOT
     }
 }
 
-template <typename T> __device__ __forceinline__ T rcp_nr(T p) {
-    // reciprocal: hardware estimate + two Newton steps (full precision)
-    T r;
-    if constexpr (sizeof(T) == 8) r = __builtin_amdgcn_rcp(p); else r = __builtin_amdgcn_rcpf(p);
-    r = fma(r, fma(-p, r, T(1)), r);
-    r = fma(r, fma(-p, r, T(1)), r);
-    return r;
-}
 
-// (4) block-Thomas factorization of S with explicit symmetric inverses (wave 0, all 64 lanes):
-//   I_0 = S_00^-1;  X_j = S_{j-1,j}' I_{j-1};  I_j = (S_jj - X_j S_{j-1,j})^-1
-// Sd[j] <- I_j, So[j-1] <- X_j.  Inverses by Gauss-Jordan sweeps (SPD: no pivoting), with a
-// pivot floor (near the solution of a degenerate QP the last Schur blocks are differences of
-// O(M) numbers and may lose positivity by rounding).
-template <typename T> __device__ void seq_factor(T *Sd, T *So, int NB, T *sh) {
+// (4) two-ended ("twisted") block-Thomas factorization of the SPD block-tridiagonal S with
+// explicit symmetric inverses.  Wave 0 eliminates from the top, wave 1 from the bottom, and the
+// two meet at block m:
+//   top    (j < m):  X_j = S_{j,j-1} I_{j-1},  I_j = (S_jj - X_j S_{j-1,j})^-1      So[j-1] <- X_j
+//   bottom (j > m):  Y_j = S_{j,j+1} I_{j+1},  I_j = (S_jj - Y_j S_{j+1,j})^-1      So[j]   <- Y_j
+//   meet   (j = m):  I_m = (S_mm - X_m S_{m-1,m} - Y_m S_{m+1,m})^-1
+// Sd[j] <- I_j.  So[j] holds S_{j,j+1} on input.  Inverses by Gauss-Jordan sweeps over the 64
+// lanes (SPD: no pivoting) with a pivot floor relative to the original diagonal (near the
+// solution of a degenerate QP the Schur blocks are differences of O(M) numbers).
+template <typename T, typename PS> __device__ void tw_block(PS *Sd, PS *So, int j, bool top, bool bot, LdsT<T> *sh) {
     const int lane = threadIdx.x & 63;
-    T *A = sh, *Xb = sh + 96;
+    LdsT<T> *A = sh, *Xb = sh + 96;
     const int e0 = lane, e1 = lane + 64;
     const bool has1 = e1 < 81;
     const int i0 = e0 / 9, c0 = e0 % 9, i1 = e1 / 9, c1 = e1 % 9;
-    for (int j = 0; j < NB; ++j) {
-        T *Dj = Sd + (size_t)j * 81;
-        if (j == 0) {
-            A[e0] = Dj[e0];
-            if (has1) A[e1] = Dj[e1];
-        } else {
-            const T *Ip = Sd + (size_t)(j - 1) * 81, *Op = So + (size_t)(j - 1) * 81;
-            T x0 = T(0), x1 = T(0);
-            for (int m = 0; m < 9; ++m) {
-                x0 = fma(Op[m * 9 + i0], Ip[m * 9 + c0], x0);
-                if (has1) x1 = fma(Op[m * 9 + i1], Ip[m * 9 + c1], x1);
-            }
-            Xb[e0] = x0;
-            if (has1) Xb[e1] = x1;
-            wave_sync();
-            T a0 = Dj[e0], a1 = has1 ? Dj[e1] : T(0);
-            for (int m = 0; m < 9; ++m) {
-                a0 = fma(-Xb[i0 * 9 + m], Op[m * 9 + c0], a0);
-                if (has1) a1 = fma(-Xb[i1 * 9 + m], Op[m * 9 + c1], a1);
-            }
-            wave_sync();
-            A[e0] = a0;
-            T *Ow = So + (size_t)(j - 1) * 81;
-            Ow[e0] = x0;
-            if (has1) { A[e1] = a1; Ow[e1] = x1; }
+    PS *Dj = Sd + (size_t)j * 81;
+    T a0 = Dj[e0], a1 = has1 ? Dj[e1] : T(0);
+    T x0 = T(0), x1 = T(0), y0 = T(0), y1 = T(0);
+    if (top) {   // X = So[j-1]' I_{j-1};  A -= X So[j-1]
+        const PS *Ip = Sd + (size_t)(j - 1) * 81, *Op = So + (size_t)(j - 1) * 81;
+        for (int m = 0; m < 9; ++m) {
+            x0 = fma(Op[m * 9 + i0], Ip[m * 9 + c0], x0);
+            if (has1) x1 = fma(Op[m * 9 + i1], Ip[m * 9 + c1], x1);
+        }
+        Xb[e0] = x0;
+        if (has1) Xb[e1] = x1;
+        wave_sync();
+        for (int m = 0; m < 9; ++m) {
+            a0 = fma(-Xb[i0 * 9 + m], Op[m * 9 + c0], a0);
+            if (has1) a1 = fma(-Xb[i1 * 9 + m], Op[m * 9 + c1], a1);
         }
         wave_sync();
-        for (int c = 0; c < 9; ++c) {
-            const T p = fmax(A[c * 9 + c], T(1e-13) * Dj[c * 9 + c]);
-            const T ip = rcp_nr(p);
-            const T aic0 = A[i0 * 9 + c], acj0 = A[c * 9 + c0], aij0 = A[e0];
-            T aic1 = T(0), acj1 = T(0), aij1 = T(0);
-            if (has1) { aic1 = A[i1 * 9 + c]; acj1 = A[c * 9 + c1]; aij1 = A[e1]; }
-            wave_sync();
-            auto upd = [&](int i, int cc, T aic, T acj, T aij) -> T {
-                if (i != c && cc != c) return fma(-aic * ip, acj, aij);
-                if (i == c && cc != c) return acj * ip;
-                if (i != c && cc == c) return -aic * ip;
-                return ip;
-            };
-            A[e0] = upd(i0, c0, aic0, acj0, aij0);
-            if (has1) A[e1] = upd(i1, c1, aic1, acj1, aij1);
-            wave_sync();
+    }
+    if (bot) {   // Y = So[j] I_{j+1};  A -= Y So[j]'
+        const PS *Iq = Sd + (size_t)(j + 1) * 81, *Oq = So + (size_t)j * 81;
+        for (int m = 0; m < 9; ++m) {
+            y0 = fma(Oq[i0 * 9 + m], Iq[m * 9 + c0], y0);
+            if (has1) y1 = fma(Oq[i1 * 9 + m], Iq[m * 9 + c1], y1);
         }
-        Dj[e0] = A[e0];
-        if (has1) Dj[e1] = A[e1];
+        Xb[e0] = y0;
+        if (has1) Xb[e1] = y1;
         wave_sync();
+        for (int m = 0; m < 9; ++m) {
+            a0 = fma(-Xb[i0 * 9 + m], Oq[c0 * 9 + m], a0);
+            if (has1) a1 = fma(-Xb[i1 * 9 + m], Oq[c1 * 9 + m], a1);
+        }
+        wave_sync();
+    }
+    A[e0] = a0;
+    if (has1) A[e1] = a1;
+    if (top) { PS *Ow = So + (size_t)(j - 1) * 81; Ow[e0] = x0; if (has1) Ow[e1] = x1; }
+    if (bot) { PS *Ow = So + (size_t)j * 81; Ow[e0] = y0; if (has1) Ow[e1] = y1; }
+    wave_sync();
+    for (int c = 0; c < 9; ++c) {
+        const T p = fmax(A[c * 9 + c], T(1e-13) * Dj[c * 9 + c]);
+        const T ip = rcp_nr(p);
+        const T aic0 = A[i0 * 9 + c], acj0 = A[c * 9 + c0], aij0 = A[e0];
+        T aic1 = T(0), acj1 = T(0), aij1 = T(0);
+        if (has1) { aic1 = A[i1 * 9 + c]; acj1 = A[c * 9 + c1]; aij1 = A[e1]; }
+        wave_sync();
+        auto upd = [&](int i, int cc, T aic, T acj, T aij) -> T {
+            if (i != c && cc != c) return fma(-aic * ip, acj, aij);
+            if (i == c && cc != c) return acj * ip;
+            if (i != c && cc == c) return -aic * ip;
+            return ip;
+        };
+        A[e0] = upd(i0, c0, aic0, acj0, aij0);
+        if (has1) A[e1] = upd(i1, c1, aic1, acj1, aij1);
+        wave_sync();
+    }
+    Dj[e0] = A[e0];
+    if (has1) Dj[e1] = A[e1];
+    wave_sync();
+}
+
+// the two ends (call with threads 0..127; wave 0 top blocks 0..m-1, wave 1 bottom blocks
+// NB-1..m+1); the meeting block follows after a workgroup barrier (tw_block(.., m, true, true))
+template <typename T, typename PS> __device__ void tw_factor_ends(PS *Sd, PS *So, int NB, int m, LdsT<T> *sh) {
+    if ((threadIdx.x >> 6) == 0) {
+        for (int j = 0; j < m; ++j) tw_block<T, PS>(Sd, So, j, j > 0, false, sh);
+    } else {
+        for (int j = NB - 1; j > m; --j) tw_block<T, PS>(Sd, So, j, false, j < NB - 1, sh + 192);
     }
 }
 
-// (5c) forward / backward block sweeps with the Thomas factors: rhs -> dnu
-//   y_0 = b_0, y_j = b_j - X_j y_{j-1};  x_{NB-1} = I y;  x_j = I_j y_j - X_{j+1}' x_{j+1}
-// The right-hand side and the sweep vectors are staged in LDS (vb: NB*9 elements).
-template <typename T> __device__ void seq_solve(const T *Ii, const T *Xs, const T *rhs, T *dnu, int NB, T *vb) {
+// (5c) two-ended block sweeps with the twisted factors: rhs -> dnu (vector staged in LDS vb)
+//   top:    y_0 = b_0, y_j = b_j - X_j y_{j-1}           bottom: y_j = b_j - Y_j y_{j+1}
+//   meet:   x_m = I_m (b_m - X_m y_{m-1} - Y_m y_{m+1})
+//   up:     x_j = I_j y_j - X_{j+1}' x_{j+1}  (j < m)   down: x_j = I_j y_j - Y_{j-1}' x_{j-1}  (j > m)
+// X_j sits at So[j-1], Y_j at So[j].  Three stages separated by workgroup barriers.
+template <typename T, typename PS> __device__ void tw_solve_elim(const PS *Xs, const T *rhs, int NB, int m, LdsT<T> *vb) {
     const int lane = threadIdx.x & 63;
-    for (int e = lane; e < NB * 9; e += WAVE) vb[e] = rhs[e];
+    const bool top = (threadIdx.x >> 6) == 0;
+    const int lo = top ? 0 : m + 1, hi = top ? m + 1 : NB;   // rhs blocks staged by this wave
+    for (int e = lo * 9 + lane; e < hi * 9; e += WAVE) vb[e] = rhs[e];
     wave_sync();
-    for (int j = 1; j < NB; ++j) {
-        if (lane < 9) {
-            const T *X = Xs + (size_t)(j - 1) * 81 + lane * 9;
-            const T *yp = vb + (size_t)(j - 1) * 9;
-            T v = vb[(size_t)j * 9 + lane];
-            for (int m = 0; m < 9; ++m) v = fma(-X[m], yp[m], v);
-            vb[(size_t)j * 9 + lane] = v;
-        }
-        wave_sync();
-    }
-    for (int j = NB - 1; j >= 0; --j) {
-        T v = T(0);
-        if (lane < 9) {
-            const T *I = Ii + (size_t)j * 81 + lane * 9;   // symmetric: row == column
-            const T *y = vb + (size_t)j * 9;
-            for (int m = 0; m < 9; ++m) v = fma(I[m], y[m], v);
-            if (j < NB - 1) {
-                const T *X = Xs + (size_t)j * 81;             // X_{j+1} stored at So[j]
-                const T *xn = vb + (size_t)(j + 1) * 9;
-                for (int m = 0; m < 9; ++m) v = fma(-X[m * 9 + lane], xn[m], v);
+    if (top) {
+        for (int j = 1; j < m; ++j) {
+            if (lane < 9) {
+                const PS *X = Xs + (size_t)(j - 1) * 81 + lane * 9;
+                const LdsT<T> *yp = vb + (size_t)(j - 1) * 9;
+                T v = vb[(size_t)j * 9 + lane];
+                for (int q = 0; q < 9; ++q) v = fma(-X[q], yp[q], v);
+                vb[(size_t)j * 9 + lane] = v;
             }
+            wave_sync();
         }
-        wave_sync();
-        if (lane < 9) vb[(size_t)j * 9 + lane] = v;
-        wave_sync();
+    } else {
+        for (int j = NB - 2; j > m; --j) {
+            if (lane < 9) {
+                const PS *Y = Xs + (size_t)j * 81 + lane * 9;
+                const LdsT<T> *yn = vb + (size_t)(j + 1) * 9;
+                T v = vb[(size_t)j * 9 + lane];
+                for (int q = 0; q < 9; ++q) v = fma(-Y[q], yn[q], v);
+                vb[(size_t)j * 9 + lane] = v;
+            }
+            wave_sync();
+        }
     }
-    for (int e = lane; e < NB * 9; e += WAVE) dnu[e] = vb[e];
+}
+template <typename T, typename PS> __device__ void tw_solve_meet(const PS *Ii, const PS *Xs, int NB, int m, LdsT<T> *vb, LdsT<T> *sh) {
+    const int lane = threadIdx.x & 63;
+    if (lane < 9) {
+        T v = vb[(size_t)m * 9 + lane];
+        const PS *X = Xs + (size_t)(m - 1) * 81 + lane * 9, *Y = Xs + (size_t)m * 81 + lane * 9;
+        const LdsT<T> *yp = vb + (size_t)(m - 1) * 9, *yn = vb + (size_t)(m + 1) * 9;
+        for (int q = 0; q < 9; ++q) v = fma(-X[q], yp[q], fma(-Y[q], yn[q], v));
+        sh[lane] = v;
+    }
+    wave_sync();
+    if (lane < 9) {
+        const PS *I = Ii + (size_t)m * 81 + lane * 9;
+        T v = T(0);
+        for (int q = 0; q < 9; ++q) v = fma(I[q], sh[q], v);
+        vb[(size_t)m * 9 + lane] = v;
+    }
+    wave_sync();
+}
+template <typename T, typename PS> __device__ void tw_solve_back(const PS *Ii, const PS *Xs, T *dnu, int NB, int m, LdsT<T> *vb) {
+    const int lane = threadIdx.x & 63;
+    const bool top = (threadIdx.x >> 6) == 0;
+    if (top) {
+        for (int j = m - 1; j >= 0; --j) {
+            T v = T(0);
+            if (lane < 9) {
+                const PS *I = Ii + (size_t)j * 81 + lane * 9;  // symmetric: row == column
+                const LdsT<T> *y = vb + (size_t)j * 9;
+                for (int q = 0; q < 9; ++q) v = fma(I[q], y[q], v);
+                const PS *X = Xs + (size_t)j * 81;             // X_{j+1} at So[j]
+                const LdsT<T> *xn = vb + (size_t)(j + 1) * 9;
+                for (int q = 0; q < 9; ++q) v = fma(-X[q * 9 + lane], xn[q], v);
+            }
+            wave_sync();
+            if (lane < 9) vb[(size_t)j * 9 + lane] = v;
+            wave_sync();
+        }
+    } else {
+        for (int j = m + 1; j < NB; ++j) {
+            T v = T(0);
+            if (lane < 9) {
+                const PS *I = Ii + (size_t)j * 81 + lane * 9;
+                const LdsT<T> *y = vb + (size_t)j * 9;
+                for (int q = 0; q < 9; ++q) v = fma(I[q], y[q], v);
+                const PS *Y = Xs + (size_t)(j - 1) * 81;       // Y_{j-1} at So[j-1]
+                const LdsT<T> *xp = vb + (size_t)(j - 1) * 9;
+                for (int q = 0; q < 9; ++q) v = fma(-Y[q * 9 + lane], xp[q], v);
+            }
+            wave_sync();
+            if (lane < 9) vb[(size_t)j * 9 + lane] = v;
+            wave_sync();
+        }
+    }
+    const int lo = top ? 0 : m, hi = top ? m : NB;
+    for (int e = lo * 9 + lane; e < hi * 9; e += WAVE) dnu[e] = vb[e];
 }
 
 // r_hat = r_i - r_c / lambda for the rows of knot k  (rc supplied per mode)
@@ -719,7 +805,7 @@ __device__ void rhat_rows(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu, T
         if (!C.present(k, r)) { rh[r] = T(0); continue; }
         T rc = s[r] * lm[r];
         if (corr) rc += dsa[r] * dla[r] - sigma_mu;
-        rh[r] = rdi[r] - rc / lm[r];
+        rh[r] = rdi[r] - fdiv(rc, lm[r]);
     }
 }
 
@@ -869,8 +955,8 @@ __device__ T phase_dz(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu) {
     }
     for (int r = 0; r < NI; ++r) {
         if (!C.present(k, r)) continue;
-        if (ds[r] < T(0)) amax = fmin(amax, -s[r] / ds[r]);
-        if (dl[r] < T(0)) amax = fmin(amax, -lm[r] / dl[r]);
+        if (ds[r] < T(0)) amax = fmin(amax, fdiv(-s[r], ds[r]));
+        if (dl[r] < T(0)) amax = fmin(amax, fdiv(-lm[r], dl[r]));
     }
     return amax;
 }
@@ -948,8 +1034,8 @@ __global__ void __launch_bounds__(NT) k_qp_ipm(DevBuf<T> d, int only_active, int
     if (b >= d.B) return;
     if (only_active && !d.scp[b].active) return;
     __shared__ T red[8 * (NT / 64)];
-    __shared__ T sh[256];
-    const int tid = threadIdx.x, N = d.N, K1 = N + 1, NB = N + 2;
+    __shared__ T sh[512];
+    const int tid = threadIdx.x, N = d.N, K1 = N + 1, NB = N + 2, NBm = NB / 2;
     Ctx<T, ROBOT> C{N, nullptr, nullptr, nullptr, nullptr, T(0), T(0), nullptr, WsLayout(N, NI, Robot<ROBOT>::NC),
                     nullptr, nullptr, T(0)};
     C.prm = d.params + d.class_id[b];
@@ -965,6 +1051,7 @@ __global__ void __launch_bounds__(NT) k_qp_ipm(DevBuf<T> d, int only_active, int
     }
     C.ws = d.ws + (size_t)b * d.ws_stride;
     T *vbuf = reinterpret_cast<T *>(dsmem);
+    LdsT<T> *vbl = (LdsT<T> *)vbuf, *shl = (LdsT<T> *)sh;
     if (SL) {
         C.Sd = vbuf + (((size_t)NB * 9 + 7) & ~size_t(7));
         C.So = C.Sd + (size_t)NB * 81;
@@ -1034,7 +1121,15 @@ __global__ void __launch_bounds__(NT) k_qp_ipm(DevBuf<T> d, int only_active, int
         for (int k = tid; k < K1; k += NT) phase_sblock<T, ROBOT>(C, k);
         __syncthreads();
         STAMP(2);
-        if (tid < 64) seq_factor(C.Sd, C.So, NB, sh);
+        if (SL) {
+            if (tid < 128) tw_factor_ends<T, LdsT<T>>((LdsT<T> *)C.Sd, (LdsT<T> *)C.So, NB, NBm, shl);
+            __syncthreads();
+            if (tid < 64) tw_block<T, LdsT<T>>((LdsT<T> *)C.Sd, (LdsT<T> *)C.So, NBm, true, true, shl);
+        } else {
+            if (tid < 128) tw_factor_ends<T, T>(C.Sd, C.So, NB, NBm, shl);
+            __syncthreads();
+            if (tid < 64) tw_block<T, T>(C.Sd, C.So, NBm, true, true, shl);
+        }
         STAMP(3);
         __syncthreads();
         // ---- predictor (affine) and corrector
@@ -1047,7 +1142,20 @@ __global__ void __launch_bounds__(NT) k_qp_ipm(DevBuf<T> d, int only_active, int
             for (int k = tid; k < K1; k += NT) phase_rhs<T, ROBOT>(C, k);
             __syncthreads();
             STAMP(5);
-            if (tid < 64) seq_solve(C.Sd, C.So, C.ws + C.L.rhs, C.ws + C.L.dnu, NB, vbuf);
+            if (SL) {
+                LdsT<T> *Sd = (LdsT<T> *)C.Sd, *So = (LdsT<T> *)C.So;
+                if (tid < 128) tw_solve_elim<T, LdsT<T>>(So, C.ws + C.L.rhs, NB, NBm, vbl);
+                __syncthreads();
+                if (tid < 64) tw_solve_meet<T, LdsT<T>>(Sd, So, NB, NBm, vbl, shl);
+                __syncthreads();
+                if (tid < 128) tw_solve_back<T, LdsT<T>>(Sd, So, C.ws + C.L.dnu, NB, NBm, vbl);
+            } else {
+                if (tid < 128) tw_solve_elim<T, T>(C.So, C.ws + C.L.rhs, NB, NBm, vbl);
+                __syncthreads();
+                if (tid < 64) tw_solve_meet<T, T>(C.Sd, C.So, NB, NBm, vbl, shl);
+                __syncthreads();
+                if (tid < 128) tw_solve_back<T, T>(C.Sd, C.So, C.ws + C.L.dnu, NB, NBm, vbl);
+            }
             __syncthreads();
             STAMP(6);
             T am[1] = {T(1)};

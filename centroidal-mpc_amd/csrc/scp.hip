@@ -173,6 +173,26 @@ __global__ void __launch_bounds__(256) k_accept(DevBuf<T> d, int fixed_iters) {
     for (int e = tid; e < K1 * 81; e += 256) d.Sacc[(size_t)b * K1 * 81 + e] = d.Sig[(size_t)b * K1 * 81 + e];
 }
 
+// nonlinear rollout x+_k = x_k + dt F(x_k, u_k) along (X, U) for k = 0..N (reference
+// integrate_dynamics_trajectory, src/centroidal_model.py:243-255; at k = N the reference's JAX
+// gathers clamp to the last control / contact row, quirk Q9).  One thread per (problem, knot).
+template <typename T, int ROBOT>
+__global__ void __launch_bounds__(128) k_rollout(DevBuf<T> d, const T *X, const T *U, T *out) {
+    constexpr int NC = Robot<ROBOT>::NC;
+    const int N = d.N, K1 = N + 1;
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long)d.B * K1) return;
+    const int b = (int)(i / K1), k = (int)(i % K1), kc = k < N ? k : N - 1;
+    const size_t kn = (size_t)b * N + kc;
+    step_dyn<T, ROBOT>(d.params[d.class_id[b]], X + (size_t)i * 9, U + kn * NU, d.pos + kn * 3 * NC, d.rot + kn * 9 * NC,
+                       d.logic + kn * NC, out + (size_t)i * 9);
+}
+
+template __global__ void k_rollout<double, 0>(DevBuf<double>, const double *, const double *, double *);
+template __global__ void k_rollout<double, 1>(DevBuf<double>, const double *, const double *, double *);
+template __global__ void k_rollout<float, 0>(DevBuf<float>, const float *, const float *, float *);
+template __global__ void k_rollout<float, 1>(DevBuf<float>, const float *, const float *, float *);
+
 template __global__ void k_accept<double, 0>(DevBuf<double>, int);
 template __global__ void k_accept<double, 1>(DevBuf<double>, int);
 template __global__ void k_accept<float, 0>(DevBuf<float>, int);

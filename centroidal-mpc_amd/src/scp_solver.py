@@ -1,0 +1,196 @@
+"""Sequential convex programming driver (drop-in for reference src/scp_solver.py:1-179).
+
+Same public functions, arguments and return types as the reference; the work runs in
+libcmpc.so on the GPU:
+
+* ``solve_scp(model, scp_params)`` runs the whole GuSTO-style loop on the device
+  (cmpc_solve_scp: linearize -> assemble -> batched interior-point QP -> trust-region test and
+  accept/reject per iteration) and returns the reference's dict of accepted solutions, or
+  False when a QP subproblem fails (quirk Q13).
+* ``solve_scp_batch(models, ...)`` is the batched entry: many models (one robot / horizon) in one
+  device handle, one result per model.
+* ``sum_up_all_costs`` / ``stack_up_all_constraints`` / ``solve_subproblem`` keep the reference's
+  step-by-step interface.  The QP they describe is the one assembled on the device, exported
+  in the reference's CSC layout; ``solve_subproblem`` solves it with the device QP solver
+  (structure-exploiting, so it accepts the QPs these two functions built, not arbitrary CSC).
+
+The reference's OSQP call (eps 1e-7 + polish, src/scp_solver.py:59-68) is replaced by an
+interior-point method converged to 1e-11 (fp64): the QP's minimizer is unique (P > 0 on the
+states and controls, slacks priced linearly), so both return the same solution to within the
+reference's own tolerance.
+"""
+from collections import namedtuple
+from warnings import warn
+
+import numpy as np
+
+from cmpc._lib import Solver
+from cmpc.problem import ProblemBatch
+from src import _device
+from src.constraints import Constraint
+from src.cost import Cost
+
+Info = namedtuple('Info', 'status status_val iter obj_val')
+Result = namedtuple('Result', 'x y info')
+
+# device QP status -> OSQP status strings (the reference compares res.info.status to 'solved')
+QP_STATUS = {1: 'solved', 2: 'solved inaccurate', -2: 'maximum iterations reached', -3: 'primal infeasible',
+             -4: 'dual infeasible', -10: 'unsolved'}
+SCP_QP_FAILED = -1
+
+
+class _DeviceCost(Cost):
+    """Cost(Q, p) that remembers the model whose device assembly produced it."""
+
+
+class _DeviceConstraint(Constraint):
+    """Constraint(mat, lb, ub) that remembers the device state that produced it."""
+
+
+def sum_up_all_costs(model):
+    """P, q of the SCP subproblem (reference :10-26)."""
+    _, P, q, _, _, _ = _device.export(model)
+    c = _DeviceCost(Q=P, p=q)
+    c._model = model
+    return c
+
+
+def stack_up_all_constraints(model, traj_tuple, traj_data, trust_region_updates):
+    """A, l, u in the reference's row order (reference :28-48).  ``traj_data`` is accepted for
+    signature compatibility; the device linearizes at ``traj_tuple`` itself."""
+    tr = {'weight': float(np.asarray(trust_region_updates['weight'])),
+          'radius': float(np.asarray(trust_region_updates['radius']))}
+    _, _, _, A, l, u = _device.export(model, traj_tuple, tr)
+    c = _DeviceConstraint(mat=A, lb=l, ub=u)
+    c._model, c._traj, c._tr = model, traj_tuple, tr
+    return c
+
+
+def convergence(traj_tuple_curr, traj_tuple_prev):
+    """Relative spectral-norm change (reference :51-56)."""
+    X_prev, U_prev = traj_tuple_prev['state'], traj_tuple_prev['control']
+    X_curr, U_curr = traj_tuple_curr['state'], traj_tuple_curr['control']
+    return (np.linalg.norm(U_curr - U_prev, 2) / np.linalg.norm(U_curr, 2) +
+            np.linalg.norm(X_curr - X_prev, 2) / np.linalg.norm(X_curr, 2))
+
+
+def solve_subproblem(cost, constraints):
+    """Solve the QP built by sum_up_all_costs / stack_up_all_constraints on the device;
+    returns (QP_FEASIBILITY, res) with res.x, res.y, res.info.status as OSQP's (reference :59-68)."""
+    model = getattr(constraints, '_model', None)
+    if model is None:
+        raise NotImplementedError('solve_subproblem solves the QPs assembled by stack_up_all_constraints (the '
+                                  'device solver exploits their stage structure); arbitrary CSC QPs are not '
+                                  'supported')
+    s, P, q, A, l, u = _device.export(model, constraints._traj, constraints._tr)
+    if getattr(cost, '_model', None) is not model:
+        if (cost.Q.shape != P.shape or abs(cost.Q - P).max() > 0 or
+                np.abs(np.asarray(cost.p) - q).max() > 1e-12 * max(1.0, np.abs(q).max())):
+            raise ValueError('the cost does not match the device assembly of this model')
+    s.qp_solve()
+    z, y, st, it = s.qp_solution()
+    x = z[0]
+    status = QP_STATUS.get(int(st[0]), 'unsolved')
+    res = Result(x=x, y=y[0], info=Info(status, int(st[0]), int(it[0]), float(0.5 * x @ (P @ x) + q @ x)))
+    if status != 'solved':
+        warn('[solve_OSQP]: Problem unfeasible.')
+        return False, res
+    return True, res
+
+
+def compute_model_accuracy(model, curr_traj, prev_traj, prev_traj_data):
+    """rho = sum_k |x+(X_k, U_k)[6:] - lin_k[6:]|^2 / sum_k |lin_k|^2 with
+    lin_k = f_k + A_k dx_k + B_k du_k over k < N (reference :71-87); the rollout runs on the device."""
+    nl = model.integrate_dynamics_trajectory(curr_traj)
+    N = model._N
+    f = np.asarray(prev_traj_data['dynamics'])[:, :N]
+    A = np.asarray(prev_traj_data['gradients']['f_x'])
+    B = np.asarray(prev_traj_data['gradients']['f_u'])
+    dX = (np.asarray(curr_traj['state']) - np.asarray(prev_traj['state']))[:, :N]
+    dU = (np.asarray(curr_traj['control']) - np.asarray(prev_traj['control']))[:, :N]
+    lin = f.T + np.einsum('kij,jk->ki', A, dX) + np.einsum('kij,jk->ki', B, dU)
+    err = nl[6:, :N].T - lin[:, 6:]
+    return float((err ** 2).sum() / (lin ** 2).sum())
+
+
+def get_QP_solution(model, res):
+    """X (nx, N+1), U (nu, N) from z (reference :89-93, Fortran-order reshapes)."""
+    n_x, n_u, N = model._n_x, model._n_u, model._N
+    X_sol = np.reshape(res.x[:n_x * (N + 1)], (n_x, N + 1), order='F')
+    U_sol = np.reshape(res.x[n_x * (N + 1):n_x * (N + 1) + n_u * N], (n_u, N), order='F')
+    return dict(state=X_sol, control=U_sol)
+
+
+def interpolate_SCP_solution(solution):
+    """Linear interpolation of the last accepted solution, 10 sub-steps per interval
+    (reference :95-111): column i*10 + j = v_i + j (v_{i+1} - v_i) / 10, the last knot dropped."""
+    N_inner = 10
+    X, U = np.asarray(solution['state'][-1]), np.asarray(solution['control'][-1])
+
+    def interp(V):
+        d = (V[:, 1:] - V[:, :-1]) / float(N_inner)
+        j = np.arange(N_inner, dtype=float)
+        out = V[:, :-1, None] + d[:, :, None] * j[None, None, :]
+        return out.reshape(V.shape[0], -1)
+    return dict(X=interp(X), U=interp(U))
+
+
+def _results(sol, nu, B):
+    out = []
+    for b in range(B):
+        if int(sol['status'][b]) == SCP_QP_FAILED:
+            out.append(False)
+            continue
+        r = dict(state=[], control=[], gains=[], covs=[])
+        if int(sol['n_accepted'][b]) > 0:
+            r['state'].append(sol['X'][b].T.copy())
+            r['control'].append(sol['U'][b][:, :nu].T.copy())
+            r['gains'].append(sol['K'][b][:, :nu, :].copy())
+            r['covs'].append(sol['Sigma'][b].copy())
+        out.append(r)
+    return out
+
+
+def solve_scp(model, scp_params):
+    """The reference's SCP loop for one model (reference :118-179), run on the device."""
+    s = model._device_solver(None, scp_params)
+    s.solve_scp(fixed_iters=False)
+    sol = s.solution()
+    log = s.iteration_log()
+    res = _results(sol, model._n_u, 1)[0]
+    it = int(sol['iterations'][0])
+    if res is False:
+        print('QP subproblem Failed at iter #' + str(it - 1))
+        return False
+    print('[solve_ccscp] Success: ' + str(int(log['decision'][0]) == 1) + ', Nb of iterations: ' + str(it))
+    return res
+
+
+def solve_scp_batch(models, scp_params=None, precision='fp64', device=0, fixed_iters=False):
+    """Batched SCP: all ``models`` (one robot and horizon) in one device handle; returns one
+    result per model (the reference's dict or False).  ``scp_params`` (optional) overrides every
+    model's conf scp_params."""
+    models = list(models)
+    if not models:
+        return []
+    m0 = models[0]
+    if any(m._robot != m0._robot or m._N != m0._N for m in models):
+        raise ValueError('solve_scp_batch needs models of one robot and horizon')
+    pbs = [m.problem_batch(None, scp_params) for m in models]
+    # one parameter class per distinct conf parameter set (models built from one conf share it)
+    classes, index, cid = [], {}, np.zeros(len(models), np.int32)
+    for b, (m, pb) in enumerate(zip(models, pbs)):
+        key = id(m._params)
+        if key not in index:
+            index[key] = len(classes)
+            classes.append(pb.params[0])
+        cid[b] = index[key]
+    cat = lambda name: np.concatenate([getattr(pb, name) for pb in pbs])
+    batch = ProblemBatch(m0._robot, m0._N, pbs[0].nc, m0._n_u, cat('logic'), cat('pos'), cat('rot'), cat('Xbar'),
+                         cat('Ubar'), cid, classes)
+    batch.validate()
+    with Solver(m0._robot, m0._N, batch.B, precision, device) as s:
+        s.upload(batch)
+        s.solve_scp(fixed_iters=fixed_iters)
+        sol = s.solution()
+    return _results(sol, m0._n_u, batch.B)

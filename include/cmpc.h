@@ -104,6 +104,16 @@ int cmpc_set_params(cmpc_handle h, int n_classes, const cmpc_params *classes);
 int cmpc_upload(cmpc_handle h, int B, const int32_t *class_id, const int8_t *logic, const double *pos,
                 const double *rot, const double *Xbar, const double *Ubar);
 
+/* Override the per-problem trust-region weight / radius (B entries each; NULL keeps the current
+ * values).  Replaces the trust_region_updates={'weight','radius'} argument of
+ * stack_up_all_constraints (reference src/scp_solver.py:28, src/constraints.py:260). */
+int cmpc_set_trust_region(cmpc_handle h, const double *weight, const double *radius);
+
+/* Nonlinear rollout of the uploaded problems' dynamics along (X (B,N+1,9), U (B,N,nu)) into
+ * out (B,N+1,9); the contact data of the last knot is reused at k = N.  Replaces
+ * Centroidal_model.integrate_dynamics_trajectory (reference src/centroidal_model.py:243-255). */
+int cmpc_rollout(cmpc_handle h, const double *X, const double *U, double *out);
+
 /* ---- hot-path phases (asynchronous) ---- */
 int cmpc_linearize(cmpc_handle h);                 /* f, A, Bu, C, K, Sigma for all problems */
 int cmpc_assemble(cmpc_handle h);                  /* structured QP from linearization + SCP state */

@@ -42,3 +42,30 @@ def same_bounds(a, b, tol=1e-12):
     fin = np.isfinite(a) & np.isfinite(b)
     return bool(np.all(np.isfinite(a) == np.isfinite(b)) and np.all(np.sign(a[~fin]) == np.sign(b[~fin]))
                 and np.allclose(a[fin], b[fin], rtol=tol, atol=tol))
+
+
+def dropin_model(cfg, N, seed=0, stochastic=False, precision='fp64'):
+    """A drop-in ``Centroidal_model`` built from the config module with the horizon truncated to N
+    (the reference's behaviour when conf.N < plan length) and a synthetic warm start passed as
+    ``init_trajectories`` (the DDP npz of the reference is not available)."""
+    import types
+    from cmpc.synth import CONFIGS, warm_start, warm_start_controls
+    from src.centroidal_model import Centroidal_model
+    from src.contact_plan import create_contact_trajectory, contact_arrays
+    conf0 = load_conf(cfg)
+    conf = types.SimpleNamespace(**{k: getattr(conf0, k) for k in dir(conf0) if not k.startswith('__')})
+    conf.N = N
+    logic, pos, rot = contact_arrays(create_contact_trajectory(conf), N)
+    p = ModelParams.from_conf(conf)
+    rng = np.random.default_rng(1000 * CONFIGS[cfg][1] + seed)
+    com_z = 0.24 if p.robot == 'solo12' else 0.87
+    X = warm_start(conf, logic, pos, rng, p.mass, com_z, p.gravity, p.robot)
+    U = warm_start_controls(logic, p.mass, p.gravity, conf.n_u)
+    model = Centroidal_model(conf, STOCHASTIC_OCP=stochastic, init_trajectories=dict(state=X.T, control=U.T),
+                             precision=precision)
+    return model
+
+
+def model_oracle_problem(model):
+    """The oracle's problem dict for a drop-in model."""
+    return model.problem_batch().oracle_problem(0)
