@@ -209,18 +209,19 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
         break;
     }
     case 2: {
-        // Schur blocks in LDS when they fit beside the kernel's static LDS (one workgroup per CU)
+        // Schur inverses in LDS when they fit beside the kernel's static LDS (at N = 100 fp64 two
+        // workgroups share a CU)
         const size_t vec = ipm_vec_lds_bytes(h->N, (int)sizeof(T));
         const size_t lds = vec + ipm_schur_lds_bytes(h->N, (int)sizeof(T));
         if (lds <= 150 * 1024) {
             HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_qp_ipm<T, R, true>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            hipLaunchKernelGGL((k_qp_ipm<T, R, true>), dim3(B), dim3(256), lds, h->stream, d, only_active,
+            hipLaunchKernelGGL((k_qp_ipm<T, R, true>), dim3(B), dim3(IPM_NT), lds, h->stream, d, only_active,
                                h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), T(h->qs.step_fraction));
         } else {
             HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_qp_ipm<T, R, false>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)vec));
-            hipLaunchKernelGGL((k_qp_ipm<T, R, false>), dim3(B), dim3(256), vec, h->stream, d, only_active,
+            hipLaunchKernelGGL((k_qp_ipm<T, R, false>), dim3(B), dim3(IPM_NT), vec, h->stream, d, only_active,
                                h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), T(h->qs.step_fraction));
         }
         break;

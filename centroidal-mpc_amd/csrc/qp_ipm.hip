@@ -20,7 +20,7 @@
 
 namespace cmpc {
 
-constexpr int NT = 256;
+constexpr int NT = IPM_NT;   // two waves: the two ends of the Schur sweeps; knots k, k + 128, ...
 constexpr int FU = 34;   // per-contact factor record: Gw 12 | Kinv 10 | F 6 | Winvd 6
 // per-knot (x, t) factor record: 1/Wx[0:6] | M_LL packed 6 | chol(K_TR) packed 36 (diagonal as 1/L_jj) | z1 = L^-1 1 (8) |
 // 1/den | D_slack  (K_TR = D_TR^-1 + G_L W_L^-1 G_L', see phase_factor)
@@ -624,20 +624,23 @@ template <typename T, int ROBOT> __device__ void phase_sblock(const Ctx<T, ROBOT
 //   top    (j < m):  X_j = S_{j,j-1} I_{j-1},  I_j = (S_jj - X_j S_{j-1,j})^-1      So[j-1] <- X_j
 //   bottom (j > m):  Y_j = S_{j,j+1} I_{j+1},  I_j = (S_jj - Y_j S_{j+1,j})^-1      So[j]   <- Y_j
 //   meet   (j = m):  I_m = (S_mm - X_m S_{m-1,m} - Y_m S_{m+1,m})^-1
-// Sd[j] <- I_j.  So[j] holds S_{j,j+1} on input.  Inverses by Gauss-Jordan sweeps over the 64
-// lanes (SPD: no pivoting) with a pivot floor relative to the original diagonal (near the
+// Sd[j] <- I_j (LDS when it fits: the inverses are re-read by every sweep); So[j] holds
+// S_{j,j+1} on input and lives in global memory: each step stages the raw block it needs into
+// LDS scratch from registers loaded one step ahead.  Inverses by Gauss-Jordan sweeps over the
+// 64 lanes (SPD: no pivoting) with a pivot floor relative to the original diagonal (near the
 // solution of a degenerate QP the Schur blocks are differences of O(M) numbers).
-template <typename T, typename PS> __device__ void tw_block(PS *Sd, PS *So, int j, bool top, bool bot, LdsT<T> *sh) {
+template <typename T, typename PS>
+__device__ __forceinline__ void tw_step(PS *Sd, const LdsT<T> *Op, const LdsT<T> *Oq, T *OwTop, T *OwBot, int j,
+                                        LdsT<T> *A, LdsT<T> *Xb) {
     const int lane = threadIdx.x & 63;
-    LdsT<T> *A = sh, *Xb = sh + 96;
     const int e0 = lane, e1 = lane + 64;
     const bool has1 = e1 < 81;
     const int i0 = e0 / 9, c0 = e0 % 9, i1 = e1 / 9, c1 = e1 % 9;
     PS *Dj = Sd + (size_t)j * 81;
     T a0 = Dj[e0], a1 = has1 ? Dj[e1] : T(0);
     T x0 = T(0), x1 = T(0), y0 = T(0), y1 = T(0);
-    if (top) {   // X = So[j-1]' I_{j-1};  A -= X So[j-1]
-        const PS *Ip = Sd + (size_t)(j - 1) * 81, *Op = So + (size_t)(j - 1) * 81;
+    if (Op) {   // X = Op' I_{j-1};  A -= X Op   (Op = S_{j-1,j})
+        const PS *Ip = Sd + (size_t)(j - 1) * 81;
         for (int m = 0; m < 9; ++m) {
             x0 = fma(Op[m * 9 + i0], Ip[m * 9 + c0], x0);
             if (has1) x1 = fma(Op[m * 9 + i1], Ip[m * 9 + c1], x1);
@@ -651,8 +654,8 @@ template <typename T, typename PS> __device__ void tw_block(PS *Sd, PS *So, int 
         }
         wave_sync();
     }
-    if (bot) {   // Y = So[j] I_{j+1};  A -= Y So[j]'
-        const PS *Iq = Sd + (size_t)(j + 1) * 81, *Oq = So + (size_t)j * 81;
+    if (Oq) {   // Y = Oq I_{j+1};  A -= Y Oq'   (Oq = S_{j,j+1})
+        const PS *Iq = Sd + (size_t)(j + 1) * 81;
         for (int m = 0; m < 9; ++m) {
             y0 = fma(Oq[i0 * 9 + m], Iq[m * 9 + c0], y0);
             if (has1) y1 = fma(Oq[i1 * 9 + m], Iq[m * 9 + c1], y1);
@@ -668,8 +671,8 @@ template <typename T, typename PS> __device__ void tw_block(PS *Sd, PS *So, int 
     }
     A[e0] = a0;
     if (has1) A[e1] = a1;
-    if (top) { PS *Ow = So + (size_t)(j - 1) * 81; Ow[e0] = x0; if (has1) Ow[e1] = x1; }
-    if (bot) { PS *Ow = So + (size_t)j * 81; Ow[e0] = y0; if (has1) Ow[e1] = y1; }
+    if (Op) { OwTop[e0] = x0; if (has1) OwTop[e1] = x1; }
+    if (Oq) { OwBot[e0] = y0; if (has1) OwBot[e1] = y1; }
     wave_sync();
     for (int c = 0; c < 9; ++c) {
         const T p = fmax(A[c * 9 + c], T(1e-13) * Dj[c * 9 + c]);
@@ -693,56 +696,109 @@ template <typename T, typename PS> __device__ void tw_block(PS *Sd, PS *So, int 
     wave_sync();
 }
 
-// the two ends (call with threads 0..127; wave 0 top blocks 0..m-1, wave 1 bottom blocks
-// NB-1..m+1); the meeting block follows after a workgroup barrier (tw_block(.., m, true, true))
-template <typename T, typename PS> __device__ void tw_factor_ends(PS *Sd, PS *So, int NB, int m, LdsT<T> *sh) {
-    if ((threadIdx.x >> 6) == 0) {
-        for (int j = 0; j < m; ++j) tw_block<T, PS>(Sd, So, j, j > 0, false, sh);
+// per-wave LDS scratch of the factorization: A | Xb | Ob (96 each)
+constexpr int TW_SCRATCH = 288;
+
+// the two ends (threads 0..127: wave 0 top blocks 0..m-1, wave 1 bottom blocks NB-1..m+1)
+template <typename T, typename PS> __device__ void tw_factor_ends(PS *Sd, T *So, int NB, int m, LdsT<T> *sh) {
+    const int lane = threadIdx.x & 63;
+    const int e0 = lane, e1 = lane + 64;
+    const bool has1 = e1 < 81;
+    const bool top = (threadIdx.x >> 6) == 0;
+    LdsT<T> *A = sh + (top ? 0 : TW_SCRATCH), *Xb = A + 96, *Ob = A + 192;
+    T p0 = T(0), p1 = T(0);
+    auto fetch = [&](int blk) { p0 = So[(size_t)blk * 81 + e0]; p1 = has1 ? So[(size_t)blk * 81 + e1] : T(0); };
+    if (top) {
+        if (m > 1) fetch(0);
+        tw_step<T, PS>(Sd, nullptr, nullptr, nullptr, nullptr, 0, A, Xb);
+        for (int j = 1; j < m; ++j) {
+            Ob[e0] = p0;
+            if (has1) Ob[e1] = p1;
+            wave_sync();
+            if (j + 1 < m) fetch(j);
+            tw_step<T, PS>(Sd, Ob, nullptr, So + (size_t)(j - 1) * 81, nullptr, j, A, Xb);
+        }
     } else {
-        for (int j = NB - 1; j > m; --j) tw_block<T, PS>(Sd, So, j, false, j < NB - 1, sh + 192);
+        if (NB - 2 > m) fetch(NB - 2);
+        tw_step<T, PS>(Sd, nullptr, nullptr, nullptr, nullptr, NB - 1, A, Xb);
+        for (int j = NB - 2; j > m; --j) {
+            Ob[e0] = p0;
+            if (has1) Ob[e1] = p1;
+            wave_sync();
+            if (j - 1 > m) fetch(j - 1);
+            tw_step<T, PS>(Sd, nullptr, Ob, nullptr, So + (size_t)j * 81, j, A, Xb);
+        }
     }
+}
+
+// the meeting block (wave 0, after a workgroup barrier)
+template <typename T, typename PS> __device__ void tw_factor_meet(PS *Sd, T *So, int m, LdsT<T> *sh) {
+    const int lane = threadIdx.x & 63;
+    const int e0 = lane, e1 = lane + 64;
+    const bool has1 = e1 < 81;
+    LdsT<T> *A = sh, *Xb = A + 96, *Op = A + 192, *Oq = sh + TW_SCRATCH + 192;
+    Op[e0] = So[(size_t)(m - 1) * 81 + e0];
+    Oq[e0] = So[(size_t)m * 81 + e0];
+    if (has1) { Op[e1] = So[(size_t)(m - 1) * 81 + e1]; Oq[e1] = So[(size_t)m * 81 + e1]; }
+    wave_sync();
+    tw_step<T, PS>(Sd, Op, Oq, So + (size_t)(m - 1) * 81, So + (size_t)m * 81, m, A, Xb);
 }
 
 // (5c) two-ended block sweeps with the twisted factors: rhs -> dnu (vector staged in LDS vb)
 //   top:    y_0 = b_0, y_j = b_j - X_j y_{j-1}           bottom: y_j = b_j - Y_j y_{j+1}
 //   meet:   x_m = I_m (b_m - X_m y_{m-1} - Y_m y_{m+1})
 //   up:     x_j = I_j y_j - X_{j+1}' x_{j+1}  (j < m)   down: x_j = I_j y_j - Y_{j-1}' x_{j-1}  (j > m)
-// X_j sits at So[j-1], Y_j at So[j].  Three stages separated by workgroup barriers.
-template <typename T, typename PS> __device__ void tw_solve_elim(const PS *Xs, const T *rhs, int NB, int m, LdsT<T> *vb) {
+// X_j sits at So[j-1], Y_j at So[j] (global; lane r < 9 reads its row / column one step ahead).
+// Three stages separated by workgroup barriers.
+template <typename T> __device__ __forceinline__ void ld_row(const T *p, T (&r)[9]) {
+    for (int q = 0; q < 9; ++q) r[q] = p[q];
+}
+template <typename T> __device__ __forceinline__ void ld_col(const T *p, T (&r)[9]) {
+    for (int q = 0; q < 9; ++q) r[q] = p[q * 9];
+}
+
+template <typename T> __device__ void tw_solve_elim(const T *Xs, const T *rhs, int NB, int m, LdsT<T> *vb) {
     const int lane = threadIdx.x & 63;
     const bool top = (threadIdx.x >> 6) == 0;
+    const int lr = lane < 9 ? lane : 0;
     const int lo = top ? 0 : m + 1, hi = top ? m + 1 : NB;   // rhs blocks staged by this wave
     for (int e = lo * 9 + lane; e < hi * 9; e += WAVE) vb[e] = rhs[e];
     wave_sync();
+    T nx[9], cur[9];
     if (top) {
+        if (m > 1) ld_row(Xs + lr * 9, nx);                             // X_1 at So[0]
         for (int j = 1; j < m; ++j) {
+            for (int q = 0; q < 9; ++q) cur[q] = nx[q];
+            if (j + 1 < m) ld_row(Xs + (size_t)j * 81 + lr * 9, nx);     // X_{j+1} at So[j]
             if (lane < 9) {
-                const PS *X = Xs + (size_t)(j - 1) * 81 + lane * 9;
                 const LdsT<T> *yp = vb + (size_t)(j - 1) * 9;
                 T v = vb[(size_t)j * 9 + lane];
-                for (int q = 0; q < 9; ++q) v = fma(-X[q], yp[q], v);
+                for (int q = 0; q < 9; ++q) v = fma(-cur[q], yp[q], v);
                 vb[(size_t)j * 9 + lane] = v;
             }
             wave_sync();
         }
     } else {
+        if (NB - 2 > m) ld_row(Xs + (size_t)(NB - 2) * 81 + lr * 9, nx);     // Y_{NB-2} at So[NB-2]
         for (int j = NB - 2; j > m; --j) {
+            for (int q = 0; q < 9; ++q) cur[q] = nx[q];
+            if (j - 1 > m) ld_row(Xs + (size_t)(j - 1) * 81 + lr * 9, nx);
             if (lane < 9) {
-                const PS *Y = Xs + (size_t)j * 81 + lane * 9;
                 const LdsT<T> *yn = vb + (size_t)(j + 1) * 9;
                 T v = vb[(size_t)j * 9 + lane];
-                for (int q = 0; q < 9; ++q) v = fma(-Y[q], yn[q], v);
+                for (int q = 0; q < 9; ++q) v = fma(-cur[q], yn[q], v);
                 vb[(size_t)j * 9 + lane] = v;
             }
             wave_sync();
         }
     }
 }
-template <typename T, typename PS> __device__ void tw_solve_meet(const PS *Ii, const PS *Xs, int NB, int m, LdsT<T> *vb, LdsT<T> *sh) {
+template <typename T, typename PS>
+__device__ void tw_solve_meet(const PS *Ii, const T *Xs, int NB, int m, LdsT<T> *vb, LdsT<T> *sh) {
     const int lane = threadIdx.x & 63;
     if (lane < 9) {
         T v = vb[(size_t)m * 9 + lane];
-        const PS *X = Xs + (size_t)(m - 1) * 81 + lane * 9, *Y = Xs + (size_t)m * 81 + lane * 9;
+        const T *X = Xs + (size_t)(m - 1) * 81 + lane * 9, *Y = Xs + (size_t)m * 81 + lane * 9;
         const LdsT<T> *yp = vb + (size_t)(m - 1) * 9, *yn = vb + (size_t)(m + 1) * 9;
         for (int q = 0; q < 9; ++q) v = fma(-X[q], yp[q], fma(-Y[q], yn[q], v));
         sh[lane] = v;
@@ -756,34 +812,41 @@ template <typename T, typename PS> __device__ void tw_solve_meet(const PS *Ii, c
     }
     wave_sync();
 }
-template <typename T, typename PS> __device__ void tw_solve_back(const PS *Ii, const PS *Xs, T *dnu, int NB, int m, LdsT<T> *vb) {
+template <typename T, typename PS>
+__device__ void tw_solve_back(const PS *Ii, const T *Xs, T *dnu, int NB, int m, LdsT<T> *vb) {
     const int lane = threadIdx.x & 63;
     const bool top = (threadIdx.x >> 6) == 0;
+    const int lr = lane < 9 ? lane : 0;
+    T nx[9], cur[9];
     if (top) {
+        if (m >= 1) ld_col(Xs + (size_t)(m - 1) * 81 + lr, nx);         // X_m at So[m-1]
         for (int j = m - 1; j >= 0; --j) {
+            for (int q = 0; q < 9; ++q) cur[q] = nx[q];
+            if (j >= 1) ld_col(Xs + (size_t)(j - 1) * 81 + lr, nx);     // X_j at So[j-1]
             T v = T(0);
             if (lane < 9) {
-                const PS *I = Ii + (size_t)j * 81 + lane * 9;  // symmetric: row == column
+                const PS *I = Ii + (size_t)j * 81 + lane * 9;   // symmetric: row == column
                 const LdsT<T> *y = vb + (size_t)j * 9;
                 for (int q = 0; q < 9; ++q) v = fma(I[q], y[q], v);
-                const PS *X = Xs + (size_t)j * 81;             // X_{j+1} at So[j]
                 const LdsT<T> *xn = vb + (size_t)(j + 1) * 9;
-                for (int q = 0; q < 9; ++q) v = fma(-X[q * 9 + lane], xn[q], v);
+                for (int q = 0; q < 9; ++q) v = fma(-cur[q], xn[q], v);
             }
             wave_sync();
             if (lane < 9) vb[(size_t)j * 9 + lane] = v;
             wave_sync();
         }
     } else {
+        if (m + 1 < NB) ld_col(Xs + (size_t)m * 81 + lr, nx);            // Y_m at So[m]
         for (int j = m + 1; j < NB; ++j) {
+            for (int q = 0; q < 9; ++q) cur[q] = nx[q];
+            if (j + 1 < NB) ld_col(Xs + (size_t)j * 81 + lr, nx);       // Y_j at So[j]
             T v = T(0);
             if (lane < 9) {
                 const PS *I = Ii + (size_t)j * 81 + lane * 9;
                 const LdsT<T> *y = vb + (size_t)j * 9;
                 for (int q = 0; q < 9; ++q) v = fma(I[q], y[q], v);
-                const PS *Y = Xs + (size_t)(j - 1) * 81;       // Y_{j-1} at So[j-1]
                 const LdsT<T> *xp = vb + (size_t)(j - 1) * 9;
-                for (int q = 0; q < 9; ++q) v = fma(-Y[q * 9 + lane], xp[q], v);
+                for (int q = 0; q < 9; ++q) v = fma(-cur[q], xp[q], v);
             }
             wave_sync();
             if (lane < 9) vb[(size_t)j * 9 + lane] = v;
@@ -1034,7 +1097,7 @@ __global__ void __launch_bounds__(NT) k_qp_ipm(DevBuf<T> d, int only_active, int
     if (b >= d.B) return;
     if (only_active && !d.scp[b].active) return;
     __shared__ T red[8 * (NT / 64)];
-    __shared__ T sh[512];
+    __shared__ T sh[2 * TW_SCRATCH];
     const int tid = threadIdx.x, N = d.N, K1 = N + 1, NB = N + 2, NBm = NB / 2;
     Ctx<T, ROBOT> C{N, nullptr, nullptr, nullptr, nullptr, T(0), T(0), nullptr, WsLayout(N, NI, Robot<ROBOT>::NC),
                     nullptr, nullptr, T(0)};
@@ -1052,13 +1115,9 @@ __global__ void __launch_bounds__(NT) k_qp_ipm(DevBuf<T> d, int only_active, int
     C.ws = d.ws + (size_t)b * d.ws_stride;
     T *vbuf = reinterpret_cast<T *>(dsmem);
     LdsT<T> *vbl = (LdsT<T> *)vbuf, *shl = (LdsT<T> *)sh;
-    if (SL) {
-        C.Sd = vbuf + (((size_t)NB * 9 + 7) & ~size_t(7));
-        C.So = C.Sd + (size_t)NB * 81;
-    } else {
-        C.Sd = C.ws + C.L.Sd;
-        C.So = C.ws + C.L.So;
-    }
+    // the Schur inverses sit in LDS when they fit (SL); the off-diagonal factors always in HBM
+    C.Sd = SL ? vbuf + (((size_t)NB * 9 + 7) & ~size_t(7)) : C.ws + C.L.Sd;
+    C.So = C.ws + C.L.So;
 #ifdef CMPC_STAMPS
     unsigned long long t_prev = __builtin_amdgcn_s_memtime(), t_acc[12] = {};
 #define STAMP(i)                                                               \
@@ -1122,13 +1181,13 @@ __global__ void __launch_bounds__(NT) k_qp_ipm(DevBuf<T> d, int only_active, int
         __syncthreads();
         STAMP(2);
         if (SL) {
-            if (tid < 128) tw_factor_ends<T, LdsT<T>>((LdsT<T> *)C.Sd, (LdsT<T> *)C.So, NB, NBm, shl);
+            if (tid < 128) tw_factor_ends<T, LdsT<T>>((LdsT<T> *)C.Sd, C.So, NB, NBm, shl);
             __syncthreads();
-            if (tid < 64) tw_block<T, LdsT<T>>((LdsT<T> *)C.Sd, (LdsT<T> *)C.So, NBm, true, true, shl);
+            if (tid < 64) tw_factor_meet<T, LdsT<T>>((LdsT<T> *)C.Sd, C.So, NBm, shl);
         } else {
             if (tid < 128) tw_factor_ends<T, T>(C.Sd, C.So, NB, NBm, shl);
             __syncthreads();
-            if (tid < 64) tw_block<T, T>(C.Sd, C.So, NBm, true, true, shl);
+            if (tid < 64) tw_factor_meet<T, T>(C.Sd, C.So, NBm, shl);
         }
         STAMP(3);
         __syncthreads();
@@ -1142,16 +1201,13 @@ __global__ void __launch_bounds__(NT) k_qp_ipm(DevBuf<T> d, int only_active, int
             for (int k = tid; k < K1; k += NT) phase_rhs<T, ROBOT>(C, k);
             __syncthreads();
             STAMP(5);
+            if (tid < 128) tw_solve_elim<T>(C.So, C.ws + C.L.rhs, NB, NBm, vbl);
+            __syncthreads();
             if (SL) {
-                LdsT<T> *Sd = (LdsT<T> *)C.Sd, *So = (LdsT<T> *)C.So;
-                if (tid < 128) tw_solve_elim<T, LdsT<T>>(So, C.ws + C.L.rhs, NB, NBm, vbl);
+                if (tid < 64) tw_solve_meet<T, LdsT<T>>((LdsT<T> *)C.Sd, C.So, NB, NBm, vbl, shl);
                 __syncthreads();
-                if (tid < 64) tw_solve_meet<T, LdsT<T>>(Sd, So, NB, NBm, vbl, shl);
-                __syncthreads();
-                if (tid < 128) tw_solve_back<T, LdsT<T>>(Sd, So, C.ws + C.L.dnu, NB, NBm, vbl);
+                if (tid < 128) tw_solve_back<T, LdsT<T>>((LdsT<T> *)C.Sd, C.So, C.ws + C.L.dnu, NB, NBm, vbl);
             } else {
-                if (tid < 128) tw_solve_elim<T, T>(C.So, C.ws + C.L.rhs, NB, NBm, vbl);
-                __syncthreads();
                 if (tid < 64) tw_solve_meet<T, T>(C.Sd, C.So, NB, NBm, vbl, shl);
                 __syncthreads();
                 if (tid < 128) tw_solve_back<T, T>(C.Sd, C.So, C.ws + C.L.dnu, NB, NBm, vbl);
@@ -1218,7 +1274,7 @@ INST(float, 1)
 #undef INST
 
 size_t ipm_vec_lds_bytes(int N, int prec_bytes) { return (((size_t)(N + 2) * 9 + 7) & ~size_t(7)) * prec_bytes; }
-size_t ipm_schur_lds_bytes(int N, int prec_bytes) { return (size_t)(2 * N + 3) * 81 * prec_bytes; }
+size_t ipm_schur_lds_bytes(int N, int prec_bytes) { return (size_t)(N + 2) * 81 * prec_bytes; }
 
 size_t ipm_workspace_elems(int N, int robot) {
     return robot == 0 ? WsLayout(N, Rows<0>::NI, Robot<0>::NC).total : WsLayout(N, Rows<1>::NI, Robot<1>::NC).total;
