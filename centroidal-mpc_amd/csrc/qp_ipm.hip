@@ -29,7 +29,7 @@ constexpr int FX = 64, FX_ML = 6, FX_L = 12, FX_Z1 = 48, FX_DEN = 56, FX_DSL = 5
 // Workspace offsets (elements) for one problem.
 struct WsLayout {
     size_t s, l, x, u, t, nu, rdx, rdt, rdu, rde, rdi, facx, facu, Sd, So, wx, wt, wu, rhs, dnu, dx, dt, du,
-        ds, dl, dsa, dla, total;
+        ds, dl, dsa, dla, rh, total;
     __host__ __device__ WsLayout(int N, int NI, int NC) {
         const size_t K1 = N + 1, NB = N + 2;
         size_t o = 0;
@@ -40,6 +40,7 @@ struct WsLayout {
         So = take((N + 1) * 81); wx = take(K1 * 9); wt = take(K1); wu = take(N * NU); rhs = take(NB * 9);
         dnu = take(NB * 9); dx = take(K1 * 9); dt = take(K1); du = take(N * NU); ds = take(K1 * NI);
         dl = take(K1 * NI); dsa = take(K1 * NI); dla = take(K1 * NI);
+        rh = take(K1 * NI);
         total = o;
     }
 };
@@ -135,12 +136,26 @@ template <typename T, int ROBOT> struct Ctx {
     __device__ T Dform(T l, T s_) const { return fmin(fdiv(l, s_), dcap); }
 
     __device__ const T *st(int k) const { return stage + (size_t)k * S::SIZE; }
-    __device__ bool present(int k, int row) const {
-        if (row < R_::FR) return true;
-        if (k >= N) return false;
-        if (row < R_::CP) return logic[k * NC + (row - R_::FR) / 4] != 0;
-        return logic[k * NC + (row - R_::CP) / 4] != 0;
+    // contact-active bits of knot k, loaded once per phase (0 at k = N: only the TR rows exist)
+    __device__ unsigned cmask(int k) const {
+        if (k >= N) return 0u;
+        const uint8_t *lg = logic + (size_t)k * NC;
+        unsigned m = 0;
+        if (NC == 4) {
+            const uint32_t v = *reinterpret_cast<const uint32_t *>(lg);
+            for (int c = 0; c < 4; ++c) m |= ((v >> (8 * c)) & 0xffu) ? (1u << c) : 0u;
+        } else {
+            const uint32_t v = *reinterpret_cast<const uint16_t *>(lg);
+            for (int c = 0; c < 2; ++c) m |= ((v >> (8 * c)) & 0xffu) ? (1u << c) : 0u;
+        }
+        return m;
     }
+    __device__ static bool present_m(unsigned m, int row) {
+        if (row < R_::FR) return true;
+        if (row < R_::CP) return (m >> ((row - R_::FR) / 4)) & 1u;
+        return (m >> ((row - R_::CP) / 4)) & 1u;
+    }
+    __device__ bool present(int k, int row) const { return present_m(cmask(k), row); }
     // g'z - h of row `row` at knot k for the knot-local (x, t, u)
     __device__ T gz(int k, int row, const T *x, T t, const T *u, bool with_h) const {
         if (row < 8) {
@@ -174,8 +189,7 @@ template <typename T, int ROBOT> struct Ctx {
         gt -= v[8];
         if (k >= N) return;
         for (int i = 0; i < NU; ++i) gu[i] = T(0);
-        for (int c = 0; c < NC; ++c) {
-            if (!logic[k * NC + c]) continue;
+        for (int c = 0; c < NC; ++c) {   // rows of inactive contacts carry v = 0 and G = 0
             const T *cs = st(k) + S::CON + S::CS * c;
             for (int r = 0; r < 4; ++r) {
                 const T vr = v[R_::FR + 4 * c + r];
@@ -266,91 +280,113 @@ template <typename T> __device__ void chol8(T (&a)[36]) {
 // (1) residuals of knot k; returns norm contributions
 template <typename T, int ROBOT> struct Norms { T prim, dual, comp, mu, sp, sd, lmax, cnt; };
 
+// Per-knot phases follow load -> compute -> store: every store into the workspace comes after
+// the last load (the compiler cannot move a load above a store that may alias it, so interleaving
+// them serializes one memory round trip per row).
+template <int n, typename T, typename P> __device__ __forceinline__ void ldv(const P &p, T (&o)[n]) {
+#pragma unroll
+    for (int i = 0; i < n; ++i) o[i] = p[i];
+}
+template <int n, typename T, typename P> __device__ __forceinline__ void stv(P p, const T (&v)[n]) {
+#pragma unroll
+    for (int i = 0; i < n; ++i) p[i] = v[i];
+}
+
 template <typename T, int ROBOT> __device__ void phase_residual(const Ctx<T, ROBOT> &C, int k, Norms<T, ROBOT> &nm) {
     using S = Stage<ROBOT>;
     constexpr int NI = Rows<ROBOT>::NI;
     const int N = C.N;
+    const bool hu = k < N;
     const DevParams<T> &P = *C.prm;
-    const T *x = C.var_x(k);
-    const T t = C.ws[C.L.t + k];
-    const T *u = (k < N) ? C.var_u(k) : nullptr;
-    const T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
     const T *nu = C.ws + C.L.nu;
+    const T *st = C.st(k);
+    T x[9], u[NU], sv[NI], lm[NI];
+    ldv(C.var_x(k), x);
+    ldv(C.var_u(hu ? k : 0), u);   // k = N: no controls (values unused)
+    ldv(C.ws + C.L.s + (size_t)k * NI, sv);
+    ldv(C.ws + C.L.l + (size_t)k * NI, lm);
+    const T t = C.ws[C.L.t + k];
+    const unsigned msk = C.cmask(k);
     T lv[NI];
-    for (int r = 0; r < NI; ++r) lv[r] = C.present(k, r) ? lm[r] : T(0);
+#pragma unroll
+    for (int r = 0; r < NI; ++r) lv[r] = Ctx<T, ROBOT>::present_m(msk, r) ? lm[r] : T(0);
     T gL[3], gt, gu[NU];
     C.gtv(k, lv, gL, gt, gu);
     // E' nu at knot k
-    T ex[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    T ex[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, eu[NU];
     if (k == 0) for (int i = 0; i < 9; ++i) ex[i] += nu[i];
-    if (k < N) {
+    if (hu) {
         T a[9];
-        opAT(C.st(k) + S::W, C.beta, nu + (size_t)(1 + k) * 9, a);
+        opAT(st + S::W, C.beta, nu + (size_t)(1 + k) * 9, a);
         for (int i = 0; i < 9; ++i) ex[i] += a[i];
+        opBT<T, ROBOT>(st, nu + (size_t)(1 + k) * 9, eu);
     }
     if (k >= 1) for (int i = 0; i < 9; ++i) ex[i] -= nu[(size_t)k * 9 + i];
     if (k == N) for (int i = 0; i < 9; ++i) ex[i] += nu[(size_t)(N + 1) * 9 + i];
-    const T *qx = C.st(k) + S::QX;
-    T *rdx = C.ws + C.L.rdx + (size_t)k * 9;
+    T rdx[9];
     for (int i = 0; i < 9; ++i) {
-        const T hx = P.Wx[i] * x[i];
+        const T hx = P.Wx[i] * x[i], q = st[S::QX + i];
         const T g = (i >= 6) ? gL[i - 6] : T(0);
-        rdx[i] = hx + qx[i] + ex[i] + g;
+        rdx[i] = hx + q + ex[i] + g;
         nm.dual = fmax(nm.dual, fabs(rdx[i]));
-        nm.sd = fmax(nm.sd, fmax(fabs(hx), fmax(fabs(qx[i]), fmax(fabs(ex[i]), fabs(g)))));
+        nm.sd = fmax(nm.sd, fmax(fabs(hx), fmax(fabs(q), fmax(fabs(ex[i]), fabs(g)))));
     }
     const T rdt = T(1) + gt;
-    C.ws[C.L.rdt + k] = rdt;
     nm.dual = fmax(nm.dual, fabs(rdt));
     nm.sd = fmax(nm.sd, T(1));
-    if (k < N) {
-        T eu[NU];
-        opBT<T, ROBOT>(C.st(k), nu + (size_t)(1 + k) * 9, eu);
-        T *rdu = C.ws + C.L.rdu + (size_t)k * NU;
+    T rdu[NU], rde[9], rdb[9];
+    if (hu) {
         for (int i = 0; i < NU; ++i) {
-            const T hu = P.Wu[i] * u[i];
-            rdu[i] = hu + eu[i] + gu[i];
+            const T h = P.Wu[i] * u[i];
+            rdu[i] = h + eu[i] + gu[i];
             nm.dual = fmax(nm.dual, fabs(rdu[i]));
-            nm.sd = fmax(nm.sd, fmax(fabs(hu), fmax(fabs(eu[i]), fabs(gu[i]))));
+            nm.sd = fmax(nm.sd, fmax(fabs(h), fmax(fabs(eu[i]), fabs(gu[i]))));
         }
         // dynamics row block 1+k
-        T ax[9], bu[9];
-        opA(C.st(k) + S::W, C.beta, x, ax);
-        opB<T, ROBOT>(C.st(k), u, bu);
-        const T *x1 = C.var_x(k + 1);
-        const T *r = C.st(k) + S::R;
-        T *rde = C.ws + C.L.rde + (size_t)(1 + k) * 9;
+        T ax[9], bu[9], x1[9];
+        ldv(C.var_x(k + 1), x1);
+        opA(st + S::W, C.beta, x, ax);
+        opB<T, ROBOT>(st, u, bu);
         for (int i = 0; i < 9; ++i) {
-            const T ez = ax[i] + bu[i] - x1[i];
-            rde[i] = ez - r[i];
+            const T ez = ax[i] + bu[i] - x1[i], r = st[S::R + i];
+            rde[i] = ez - r;
             nm.prim = fmax(nm.prim, fabs(rde[i]));
-            nm.sp = fmax(nm.sp, fmax(fabs(ez), fabs(r[i])));
+            nm.sp = fmax(nm.sp, fmax(fabs(ez), fabs(r)));
         }
     }
-    if (k == 0 || k == N) {
-        const int blk = (k == 0) ? 0 : N + 1;
-        T *rde = C.ws + C.L.rde + (size_t)blk * 9;
+    const bool bnd = (k == 0 || k == N);
+    if (bnd) {
         const T *xb = C.xbar + (size_t)k * 9;
         for (int i = 0; i < 9; ++i) {
-            rde[i] = x[i] - xb[i];
-            nm.prim = fmax(nm.prim, fabs(rde[i]));
+            rdb[i] = x[i] - xb[i];
+            nm.prim = fmax(nm.prim, fabs(rdb[i]));
             nm.sp = fmax(nm.sp, fmax(fabs(x[i]), fabs(xb[i])));
         }
     }
-    T *rdi = C.ws + C.L.rdi + (size_t)k * NI;
+    T rdi[NI];
+#pragma unroll
     for (int r = 0; r < NI; ++r) {
-        if (!C.present(k, r)) { rdi[r] = T(0); continue; }
+        const bool pr = Ctx<T, ROBOT>::present_m(msk, r);
         const T g = C.gz(k, r, x, t, u, false);
         const T v = C.gz(k, r, x, t, u, true);
-        rdi[r] = v + s[r];
-        nm.prim = fmax(nm.prim, fmax(v, T(0)));
-        nm.sp = fmax(nm.sp, fmax(fabs(g), fabs(g - v)));
-        const T c = s[r] * lm[r];
+        rdi[r] = pr ? v + sv[r] : T(0);
+        const T c = pr ? sv[r] * lm[r] : T(0);
+        nm.prim = fmax(nm.prim, pr ? v : T(0));
+        nm.sp = fmax(nm.sp, pr ? fmax(fabs(g), fabs(g - v)) : T(0));
         nm.comp = fmax(nm.comp, c);
         nm.mu += c;
-        nm.cnt += T(1);
-        nm.lmax = fmax(nm.lmax, lm[r]);
+        nm.cnt += pr ? T(1) : T(0);
+        nm.lmax = fmax(nm.lmax, pr ? lm[r] : T(0));
     }
+    // stores
+    stv(C.ws + C.L.rdx + (size_t)k * 9, rdx);
+    C.ws[C.L.rdt + k] = rdt;
+    if (hu) {
+        stv(C.ws + C.L.rdu + (size_t)k * NU, rdu);
+        stv(C.ws + C.L.rde + (size_t)(1 + k) * 9, rde);
+    }
+    if (bnd) stv(C.ws + C.L.rde + (size_t)(k == 0 ? 0 : N + 1) * 9, rdb);
+    stv(C.ws + C.L.rdi + (size_t)k * NI, rdi);
 }
 
 // (2) Phi factors of knot k
@@ -864,11 +900,13 @@ __device__ void rhat_rows(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu, T
     const T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
     const T *rdi = C.ws + C.L.rdi + (size_t)k * NI;
     const T *dsa = C.ws + C.L.dsa + (size_t)k * NI, *dla = C.ws + C.L.dla + (size_t)k * NI;
+    const unsigned msk = C.cmask(k);
     for (int r = 0; r < NI; ++r) {
-        if (!C.present(k, r)) { rh[r] = T(0); continue; }
+        const bool pr = Ctx<T, ROBOT>::present_m(msk, r);
         T rc = s[r] * lm[r];
         if (corr) rc += dsa[r] * dla[r] - sigma_mu;
-        rh[r] = rdi[r] - fdiv(rc, lm[r]);
+        const T v = rdi[r] - fdiv(rc, pr ? lm[r] : T(1));
+        rh[r] = pr ? v : T(0);
     }
 }
 
@@ -877,56 +915,61 @@ template <typename T, int ROBOT> __device__ void phase_w(const Ctx<T, ROBOT> &C,
     using R_ = Rows<ROBOT>;
     constexpr int NI = R_::NI, NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
     const int N = C.N;
-    const T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
+    const bool hu = k < N;
     T rh[NI];
-    rhat_rows(C, k, corr, sigma_mu, rh);
-    const T *fx = C.ws + C.L.facx + (size_t)k * FX;
-    const T *rdx = C.ws + C.L.rdx + (size_t)k * 9;
-    T *wx = C.ws + C.L.wx + (size_t)k * 9;
-    for (int i = 0; i < 6; ++i) wx[i] = fx[i] * rdx[i];
+    rhat_rows(C, k, corr, sigma_mu, rh);   // kept for phase_dz (stored below)
+    T rdx[9], fxd[6], rdu[NU];
+    ldv(C.ws + C.L.rdx + (size_t)k * 9, rdx);
+    ldv(C.ws + C.L.facx + (size_t)k * FX, fxd);
+    if (hu) ldv(C.ws + C.L.rdu + (size_t)k * NU, rdu);
+    const T rdt = C.ws[C.L.rdt + k];
+    T wx[9], wt;
+    for (int i = 0; i < 6; ++i) wx[i] = fxd[i] * rdx[i];
     {   // (L, t): w = -(local solve with v = -r_d)
         const T vL[3] = {-rdx[6], -rdx[7], -rdx[8]};
         T dL[3], dt, dlt[8], dls;
-        tr_local(C, k, vL, -C.ws[C.L.rdt + k], rh, dL, dt, dlt, dls);
+        tr_local(C, k, vL, -rdt, rh, dL, dt, dlt, dls);
         for (int i = 0; i < 3; ++i) wx[6 + i] = -dL[i];
-        C.ws[C.L.wt + k] = -dt;
+        wt = -dt;
     }
     T ou[NU];
-    if (k < N) {
-        const T *rdu = C.ws + C.L.rdu + (size_t)k * NU;
+    if (hu) {
         T vu[NU];
         for (int i = 0; i < NU; ++i) vu[i] = rdu[i];
-        if (ROBOT == 1) {   // CoP rows (D-form, folded into W_cop)
-            for (int c = 0; c < NC; ++c) {
-                if (!C.logic[k * NC + c]) continue;
+        if (ROBOT == 1) {   // CoP rows (D-form, folded into W_cop); absent rows: lambda = 0 -> D = 0, rhat = 0
+            const T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
+            for (int c = 0; c < NC; ++c)
                 for (int dd = 0; dd < 2; ++dd) {
                     const int r0 = R_::CP + 4 * c + 2 * dd;
                     vu[NUPC * c + dd] += C.Dform(lm[r0], s[r0]) * rh[r0] - C.Dform(lm[r0 + 1], s[r0 + 1]) * rh[r0 + 1];
                 }
-            }
         }
         phi_solve_u(C, k, vu, ou);
-    }
-    if (k < N) {
         for (int c = 0; c < NC; ++c) {
-            if (!C.logic[k * NC + c]) continue;
+            // inactive contacts: Gw = 0, Kinv = I and rhat = 0, so they contribute nothing
             const T *fu = C.ws + C.L.facu + ((size_t)k * NC + c) * FU;
+            T g[22];
+            ldv(fu, g);
             T kr[4];
             for (int r = 0; r < 4; ++r) {
                 T acc = T(0);
-                for (int q = 0; q < 4; ++q) acc += fu[12 + p4(r, q)] * rh[R_::FR + 4 * c + q];
+                for (int q = 0; q < 4; ++q) acc += g[12 + p4(r, q)] * rh[R_::FR + 4 * c + q];
                 kr[r] = acc;
             }
             for (int i = 0; i < 3; ++i) {
                 T acc = T(0);
-                for (int r = 0; r < 4; ++r) acc += fu[3 * r + i] * kr[r];
+                for (int r = 0; r < 4; ++r) acc += g[3 * r + i] * kr[r];
                 ou[NUPC * c + FO + i] += acc;
             }
         }
-        T *wu = C.ws + C.L.wu + (size_t)k * NU;
-        for (int i = 0; i < NU; ++i) wu[i] = ou[i];
     }
+    // stores
+    stv(C.ws + C.L.wx + (size_t)k * 9, wx);
+    C.ws[C.L.wt + k] = wt;
+    if (hu) stv(C.ws + C.L.wu + (size_t)k * NU, ou);
+    stv(C.ws + C.L.rh + (size_t)k * NI, rh);
 }
+
 
 // (5b) Schur right-hand side blocks owned by knot k: rhs = r_e - E w
 template <typename T, int ROBOT> __device__ void phase_rhs(const Ctx<T, ROBOT> &C, int k) {
@@ -948,80 +991,111 @@ template <typename T, int ROBOT> __device__ void phase_rhs(const Ctx<T, ROBOT> &
 }
 
 // (5d) direction at knot k from dnu; returns the max step allowed by this knot's rows
+// rows of knot k: ds = -r_i - G dz; dlambda from the push-through solves (TR, slack: dlt, dls;
+// friction: Kinv (Gw v + rhat) with v = -(rdu + E'dnu_u) on the forces) or the D-form (CoP);
+// returns the largest step keeping s, lambda >= 0.  The memory operands are restrict-qualified
+// so the loads of s, lambda, r_i, the stage and the friction factors are not held behind the
+// stores of ds, dlambda.  Inactive contacts: G = Gw = 0, Kinv = I, rhat = 0 -> zero steps.
+template <typename T, int ROBOT>
+__device__ __forceinline__ T dz_rows(const Ctx<T, ROBOT> &C, int k, const T (&dx)[9], T dtt, const T (&du)[NU],
+                                     const T (&eu)[NU], const T (&dlt)[8], T dls, const T (&rh)[Rows<ROBOT>::NI],
+                                     const T *__restrict__ st, const T *__restrict__ fu, const T *__restrict__ rdu,
+                                     const T *__restrict__ rdi, const T *__restrict__ sv, const T *__restrict__ lm,
+                                     T *__restrict__ ds, T *__restrict__ dl) {
+    using S = Stage<ROBOT>;
+    using R_ = Rows<ROBOT>;
+    constexpr int NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
+    const bool hu = k < C.N;
+    const unsigned msk = C.cmask(k);
+    T amax = T(1);
+    auto emit = [&](int r, bool pr, T g, T dlr) {
+        const T dsr = pr ? -rdi[r] - g : T(0);
+        ds[r] = dsr;
+        dl[r] = dlr;
+        // branch-free ratio tests (selects keep the row loop one basic block)
+        const T qs = fdiv(-sv[r], dsr < T(0) ? dsr : T(-1)), ql = fdiv(-lm[r], dlr < T(0) ? dlr : T(-1));
+        amax = fmin(amax, fmin(dsr < T(0) ? qs : T(1), dlr < T(0) ? ql : T(1)));
+    };
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        emit(j, true, tr_sign<T>(j, 0) * dx[6] + tr_sign<T>(j, 1) * dx[7] + tr_sign<T>(j, 2) * dx[8] + C.cw * dtt,
+             dlt[j]);
+    emit(8, true, -dtt, dls);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const bool pr = hu && ((msk >> c) & 1u);
+        const T *cs = st + S::CON + S::CS * c;
+        const T *g = fu + c * FU;
+        T vf[3];
+        for (int i = 0; i < 3; ++i) vf[i] = hu ? -(rdu[NUPC * c + FO + i] + eu[NUPC * c + FO + i]) : T(0);
+        T z[4];
+        for (int r = 0; r < 4; ++r)
+            z[r] = g[3 * r] * vf[0] + g[3 * r + 1] * vf[1] + g[3 * r + 2] * vf[2] + rh[R_::FR + 4 * c + r];
+        for (int r = 0; r < 4; ++r) {
+            T acc = T(0);
+            for (int q = 0; q < 4; ++q) acc += g[12 + p4(r, q)] * z[q];
+            const T gr = cs[S::G + 3 * r] * du[NUPC * c + FO] + cs[S::G + 3 * r + 1] * du[NUPC * c + FO + 1] +
+                         cs[S::G + 3 * r + 2] * du[NUPC * c + FO + 2];
+            emit(R_::FR + 4 * c + r, pr, gr, hu ? acc : T(0));
+        }
+    }
+    if (ROBOT == 1) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const bool pr = hu && ((msk >> c) & 1u);
+            for (int q = 0; q < 4; ++q) {
+                const int r = R_::CP + 4 * c + q, dd = q / 2;
+                const T gr = (q % 2 == 0) ? du[NUPC * c + dd] : -du[NUPC * c + dd];
+                emit(r, pr, gr, pr ? C.Dform(lm[r], sv[r]) * (gr + rh[r]) : T(0));
+            }
+        }
+    }
+    return amax;
+}
+
 template <typename T, int ROBOT>
 __device__ T phase_dz(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu) {
     using S = Stage<ROBOT>;
     using R_ = Rows<ROBOT>;
     constexpr int NI = R_::NI, NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
     const int N = C.N;
+    const bool hu = k < N;
+    // E' dnu at knot k; the knot-type cases are selects over in-range blocks (one basic block)
     const T *dnu = C.ws + C.L.dnu;
-    T ex[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, eu[NU];
-    if (k == 0) for (int i = 0; i < 9; ++i) ex[i] += dnu[i];
-    if (k < N) {
-        T a[9];
-        opAT(C.st(k) + S::W, C.beta, dnu + (size_t)(1 + k) * 9, a);
-        for (int i = 0; i < 9; ++i) ex[i] += a[i];
-        opBT<T, ROBOT>(C.st(k), dnu + (size_t)(1 + k) * 9, eu);
-    }
-    if (k >= 1) for (int i = 0; i < 9; ++i) ex[i] -= dnu[(size_t)k * 9 + i];
-    if (k == N) for (int i = 0; i < 9; ++i) ex[i] += dnu[(size_t)(N + 1) * 9 + i];
-    const T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
-    const T *rdi = C.ws + C.L.rdi + (size_t)k * NI;
-    T rh[NI];
-    rhat_rows(C, k, corr, sigma_mu, rh);
-    const T *fx = C.ws + C.L.facx + (size_t)k * FX;
-    const T *rdx = C.ws + C.L.rdx + (size_t)k * 9;
+    const int kc = hu ? k : 0;   // k = N: no controls or contacts (stage / factor records unused)
+    T ex[9], eu[NU], a[9], d0[9], dk[9], dN[9];
+    opAT(C.st(k) + S::W, C.beta, dnu + (size_t)(1 + k) * 9, a);   // k = N: block N+1 (unused)
+    opBT<T, ROBOT>(C.st(kc), dnu + (size_t)(1 + kc) * 9, eu);
+    ldv(dnu, d0);
+    ldv(dnu + (size_t)k * 9, dk);
+    ldv(dnu + (size_t)(N + 1) * 9, dN);
+    for (int i = 0; i < 9; ++i)
+        ex[i] = (k == 0 ? d0[i] : T(0)) + (hu ? a[i] : T(0)) - (k >= 1 ? dk[i] : T(0)) + (k == N ? dN[i] : T(0));
+    T rh[NI], rdx[9], fxd[6], wu[NU];
+    ldv(C.ws + C.L.rh + (size_t)k * NI, rh);   // this step's rhat, from phase_w
+    ldv(C.ws + C.L.rdx + (size_t)k * 9, rdx);
+    ldv(C.ws + C.L.facx + (size_t)k * FX, fxd);
+    ldv(C.ws + C.L.wu + (size_t)kc * NU, wu);
+    const T rdt = C.ws[C.L.rdt + k];
     T dx[9], dtt, du[NU], dlt[8], dls;
-    for (int i = 0; i < 6; ++i) dx[i] = -fx[i] * (rdx[i] + ex[i]);
+    for (int i = 0; i < 6; ++i) dx[i] = -fxd[i] * (rdx[i] + ex[i]);
     {
         const T vL[3] = {-(rdx[6] + ex[6]), -(rdx[7] + ex[7]), -(rdx[8] + ex[8])};
-        tr_local(C, k, vL, -C.ws[C.L.rdt + k], rh, dx + 6, dtt, dlt, dls);
+        tr_local(C, k, vL, -rdt, rh, dx + 6, dtt, dlt, dls);
     }
-    if (k < N) {
+    {
         T au[NU];
-        phi_solve_u(C, k, eu, au);
-        const T *wu = C.ws + C.L.wu + (size_t)k * NU;
-        for (int i = 0; i < NU; ++i) du[i] = -wu[i] - au[i];
+        phi_solve_u(C, kc, eu, au);
+        for (int i = 0; i < NU; ++i) du[i] = hu ? -wu[i] - au[i] : T(0);
     }
-    T *gdx = C.ws + C.L.dx + (size_t)k * 9;
-    for (int i = 0; i < 9; ++i) gdx[i] = dx[i];
+    stv(C.ws + C.L.dx + (size_t)k * 9, dx);
     C.ws[C.L.dt + k] = dtt;
-    if (k < N) { T *gdu = C.ws + C.L.du + (size_t)k * NU; for (int i = 0; i < NU; ++i) gdu[i] = du[i]; }
-    // rows
-    T *ds = C.ws + (corr ? C.L.ds : C.L.dsa) + (size_t)k * NI;
-    T *dl = C.ws + (corr ? C.L.dl : C.L.dla) + (size_t)k * NI;
-    T amax = T(1);
-    for (int r = 0; r < NI; ++r) {
-        if (!C.present(k, r)) { ds[r] = T(0); dl[r] = T(0); continue; }
-        const T g = C.gz(k, r, dx, dtt, du, false);
-        ds[r] = -rdi[r] - g;
-        if (r < 8) dl[r] = dlt[r];
-        else if (r == 8) dl[r] = dls;
-        else if (r >= R_::CP) dl[r] = C.Dform(lm[r], s[r]) * (g + rh[r]);
-    }
-    if (k < N) {
-        // friction: dlam = Kinv (Gw v + rhat),  v = -(rdu + E'dnu_u) restricted to f
-        const T *rdu = C.ws + C.L.rdu + (size_t)k * NU;
-        for (int c = 0; c < NC; ++c) {
-            if (!C.logic[k * NC + c]) continue;
-            const T *fu = C.ws + C.L.facu + ((size_t)k * NC + c) * FU;
-            T vf[3];
-            for (int i = 0; i < 3; ++i) vf[i] = -(rdu[NUPC * c + FO + i] + eu[NUPC * c + FO + i]);
-            T z[4];
-            for (int r = 0; r < 4; ++r) z[r] = fu[3 * r] * vf[0] + fu[3 * r + 1] * vf[1] + fu[3 * r + 2] * vf[2] + rh[R_::FR + 4 * c + r];
-            for (int r = 0; r < 4; ++r) {
-                T acc = T(0);
-                for (int q = 0; q < 4; ++q) acc += fu[12 + p4(r, q)] * z[q];
-                dl[R_::FR + 4 * c + r] = acc;
-            }
-        }
-    }
-    for (int r = 0; r < NI; ++r) {
-        if (!C.present(k, r)) continue;
-        if (ds[r] < T(0)) amax = fmin(amax, fdiv(-s[r], ds[r]));
-        if (dl[r] < T(0)) amax = fmin(amax, fdiv(-lm[r], dl[r]));
-    }
-    return amax;
+    if (hu) stv(C.ws + C.L.du + (size_t)k * NU, du);
+    return dz_rows<T, ROBOT>(C, k, dx, dtt, du, eu, dlt, dls, rh, C.st(k), C.ws + C.L.facu + (size_t)kc * NC * FU,
+                             C.ws + C.L.rdu + (size_t)kc * NU, C.ws + C.L.rdi + (size_t)k * NI,
+                             C.ws + C.L.s + (size_t)k * NI, C.ws + C.L.l + (size_t)k * NI,
+                             C.ws + (corr ? C.L.ds : C.L.dsa) + (size_t)k * NI,
+                             C.ws + (corr ? C.L.dl : C.L.dla) + (size_t)k * NI);
 }
 
 template <typename T, int ROBOT> __device__ T mu_after(const Ctx<T, ROBOT> &C, int k, T a) {
@@ -1030,35 +1104,45 @@ template <typename T, int ROBOT> __device__ T mu_after(const Ctx<T, ROBOT> &C, i
     const T *ds = C.ws + C.L.dsa + (size_t)k * NI, *dl = C.ws + C.L.dla + (size_t)k * NI;
     T acc = T(0);
     for (int r = 0; r < NI; ++r)
-        if (C.present(k, r)) acc += (s[r] + a * ds[r]) * (lm[r] + a * dl[r]);
+        acc += (s[r] + a * ds[r]) * (lm[r] + a * dl[r]);   // absent rows: lambda = dl = 0
     return acc;
 }
 
 template <typename T, int ROBOT> __device__ void phase_update(const Ctx<T, ROBOT> &C, int k, T a, bool affine = false) {
     constexpr int NI = Rows<ROBOT>::NI;
     const int N = C.N;
-    T *x = C.var_x(k);
-    const T *dx = C.ws + C.L.dx + (size_t)k * 9;
-    for (int i = 0; i < 9; ++i) x[i] += a * dx[i];
-    C.ws[C.L.t + k] += a * C.ws[C.L.dt + k];
-    if (k < N) {
-        T *u = C.var_u(k);
-        const T *du = C.ws + C.L.du + (size_t)k * NU;
+    {
+        T x[9], dx[9];
+        ldv(C.var_x(k), x);
+        ldv(C.ws + C.L.dx + (size_t)k * 9, dx);
+        const T t = C.ws[C.L.t + k], dt = C.ws[C.L.dt + k];
+        T n1[9], dn1[9], n0[9], dn0[9];
+        ldv(C.ws + C.L.nu + (size_t)(1 + k) * 9, n1);        // k < N: dynamics block k; k = N: final
+        ldv(C.ws + C.L.dnu + (size_t)(1 + k) * 9, dn1);
+        if (k == 0) { ldv(C.ws + C.L.nu, n0); ldv(C.ws + C.L.dnu, dn0); }
+        T u[NU], du[NU];
+        if (k < N) { ldv(C.var_u(k), u); ldv(C.ws + C.L.du + (size_t)k * NU, du); }
+        for (int i = 0; i < 9; ++i) { x[i] += a * dx[i]; n1[i] += a * dn1[i]; n0[i] += a * dn0[i]; }
         for (int i = 0; i < NU; ++i) u[i] += a * du[i];
+        stv(C.var_x(k), x);
+        C.ws[C.L.t + k] = t + a * dt;
+        stv(C.ws + C.L.nu + (size_t)(1 + k) * 9, n1);
+        if (k == 0) stv(C.ws + C.L.nu, n0);
+        if (k < N) stv(C.var_u(k), u);
     }
-    T *nu = C.ws + C.L.nu;
-    const T *dnu = C.ws + C.L.dnu;
-    for (int i = 0; i < 9; ++i) nu[(size_t)(1 + k) * 9 + i] += a * dnu[(size_t)(1 + k) * 9 + i];   // k<N: dyn k; k==N: final
-    if (k == 0) for (int i = 0; i < 9; ++i) nu[i] += a * dnu[i];
     T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
     const T *ds = C.ws + (affine ? C.L.dsa : C.L.ds) + (size_t)k * NI;
     const T *dl = C.ws + (affine ? C.L.dla : C.L.dl) + (size_t)k * NI;
-    for (int r = 0; r < NI; ++r) {
-        if (!C.present(k, r)) continue;
-        s[r] += a * ds[r];
-        lm[r] += a * dl[r];
-    }
+    T sv[NI], dsv[NI];   // absent rows: ds = dl = 0 (s stays 1, lambda 0)
+    ldv(s, sv); ldv(ds, dsv);
+    for (int r = 0; r < NI; ++r) sv[r] += a * dsv[r];
+    T lv[NI], dlv[NI];
+    ldv(lm, lv); ldv(dl, dlv);
+    stv(s, sv);
+    for (int r = 0; r < NI; ++r) lv[r] += a * dlv[r];
+    stv(lm, lv);
 }
+
 
 // initialization step: full Newton step for z and nu; s = h - gz at the new z; lambda += dlambda.
 // vmax receives (max -s, max -lambda) over this knot's rows.
@@ -1068,7 +1152,7 @@ template <typename T, int ROBOT> __device__ void phase_init_step(const Ctx<T, RO
     const int N = C.N;
     const T *x = C.var_x(k);
     const T t = C.ws[C.L.t + k];
-    const T *u = (k < N) ? C.var_u(k) : nullptr;
+    const T *u = C.var_u(k < N ? k : 0);   // k = N: rows of u are absent (values unused)
     T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
     for (int r = 0; r < NI; ++r) {
         if (!C.present(k, r)) continue;
