@@ -43,7 +43,7 @@ def cpu_baseline(N, seconds_target=12.0):
     """Time the oracle SCP iteration on host cores (bounded sample)."""
     import multiprocessing as mp
     cores = max(1, min(16, os.cpu_count() or 1))   # the GPU box's CPU share is 16
-    n_prob = 40 * cores                              # ~10-20 s of oracle work
+    n_prob = 96 * cores                              # ~10-20 s of oracle work on the box
     from cmpc.synth import make_batch
     pb = make_batch('trot', N, n_prob, seed_offset=777)
     probs = [pb.oracle_problem(b) for b in range(n_prob)]
