@@ -13,7 +13,8 @@
 // columns), friction rows G = (F_mu R')[0:4] (src/constraints.py:171-185) and their upper
 // bounds h (0, or minus the chance-constraint back-off 2 xi G_u sqrt(K Sigma K')_uu,
 // src/constraints.py:186-214).  Thread per knot; HBM-bound: reads ~1.9 KB, writes ~1.3 KB
-// per knot at fp64.
+// per knot at fp64.  Records are stored field-major per problem (field f of knot k at
+// stage[(b * SIZE + f) * KPC + k]) so the QP kernel's per-knot loads coalesce.
 #include "common.hpp"
 
 namespace cmpc {
@@ -29,7 +30,7 @@ __global__ void __launch_bounds__(128) k_assemble(DevBuf<T> d, int only_active) 
     const ScpState &sc = d.scp[b];
     if (only_active && !sc.active) return;
     const DevParams<T> &prm = d.params[d.class_id[b]];
-    T *st = d.stage + gid * St::SIZE;
+    const SV<T> st{d.stage + (size_t)b * St::SIZE * KPC + k};   // field-major record (common.hpp)
     const T *xb = d.Xbar + gid * 9;
     const T radius = T(sc.radius);
     if (k == 0) d.cw[b] = T(-1.0 / sc.weight);
@@ -57,7 +58,7 @@ __global__ void __launch_bounds__(128) k_assemble(DevBuf<T> d, int only_active) 
     const T ml = prm.mu / sqrt(T(2));
     const T Fmu[4][3] = {{1, 0, -ml}, {-1, 0, -ml}, {0, 1, -ml}, {0, -1, -ml}};
     for (int c = 0; c < NC; ++c) {
-        T *cs = st + St::CON + St::CS * c;
+        const SV<T> cs = st + (St::CON + St::CS * c);
         const T a = T(lg[c]);
         const T *Rc = rot + 9 * c;
         const T *uc = ub + NUPC * c;

@@ -17,9 +17,8 @@
 namespace cmpc {
 template <typename T, int R> __global__ void k_linearize(DevBuf<T>, int);
 template <typename T, int R> __global__ void k_assemble(DevBuf<T>, int);
-template <typename T, int R, bool SL> __global__ void k_qp_ipm(DevBuf<T>, int, int, T, T, T);
-size_t ipm_schur_lds_bytes(int N, int prec_bytes);
-size_t ipm_vec_lds_bytes(int N, int prec_bytes);
+template <typename T, int R> __global__ void k_qp_ipm(DevBuf<T>, int, int, T, T, T);
+size_t ipm_lds_bytes(int N, int prec_bytes);
 template <typename T, int R> __global__ void k_accept(DevBuf<T>, int);
 template <typename T, int R> __global__ void k_rollout(DevBuf<T>, const T *, const T *, T *);
 size_t ipm_workspace_elems(int N, int robot);
@@ -209,21 +208,13 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
         break;
     }
     case 2: {
-        // Schur inverses in LDS when they fit beside the kernel's static LDS (at N = 100 fp64 two
-        // workgroups share a CU)
-        const size_t vec = ipm_vec_lds_bytes(h->N, (int)sizeof(T));
-        const size_t lds = vec + ipm_schur_lds_bytes(h->N, (int)sizeof(T));
-        if (lds <= 150 * 1024) {
-            HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_qp_ipm<T, R, true>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            hipLaunchKernelGGL((k_qp_ipm<T, R, true>), dim3(B), dim3(IPM_NT), lds, h->stream, d, only_active,
-                               h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), T(h->qs.step_fraction));
-        } else {
-            HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_qp_ipm<T, R, false>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)vec));
-            hipLaunchKernelGGL((k_qp_ipm<T, R, false>), dim3(B), dim3(IPM_NT), vec, h->stream, d, only_active,
-                               h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), T(h->qs.step_fraction));
-        }
+        // one workgroup per problem; three (N+2) x 9 block vectors in LDS (22 KB at N = 100 fp64),
+        // the Schur blocks in the workspace, so several problems share a CU
+        const size_t lds = ipm_lds_bytes(h->N, (int)sizeof(T));
+        HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_qp_ipm<T, R>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL((k_qp_ipm<T, R>), dim3(B), dim3(IPM_NT), lds, h->stream, d, only_active, h->qs.max_iter,
+                           T(h->qs.eps_abs), T(h->qs.eps_rel), T(h->qs.step_fraction));
         break;
     }
     case 3:
@@ -332,7 +323,7 @@ int cmpc_create(cmpc_handle *out, int device, int robot, int N, int max_batch, i
         h->Sig = h->dalloc(Bm * K1 * 81 * e);
         h->Acl = h->dalloc(Bm * N * 81 * e);
         h->Qw = h->dalloc(Bm * N * 81 * e);
-        h->stage = h->dalloc(Bm * K1 * h->SS * e);
+        h->stage = h->dalloc(Bm * KPC * h->SS * e);
         h->cw = h->dalloc(Bm * e);
         h->xs = h->dalloc(Bm * K1 * 9 * e);
         h->us = h->dalloc(Bm * N * NU * e);
@@ -557,7 +548,9 @@ int cmpc_export_qp(cmpc_handle h, int b, double *P_x, int32_t *P_i, int32_t *P_p
             else from_dev<float>(h, dst.data(), (char *)src + off * e, cnt);
         };
         std::vector<double> st, A, Bm, xb;
-        dl(st, h->stage, (size_t)b * K1 * SS, (size_t)K1 * SS);
+        const int KP = KPC;
+        dl(st, h->stage, (size_t)b * KP * SS, (size_t)KP * SS);
+        auto sf = [&](int k, int f) { return st[(size_t)f * KP + k]; };   // field-major records
         dl(A, h->A, (size_t)b * N * 81, (size_t)N * 81);
         dl(Bm, h->Bu, (size_t)b * N * 9 * NU, (size_t)N * 9 * NU);
         dl(xb, h->Xbar, (size_t)b * K1 * 9, (size_t)K1 * 9);
@@ -584,7 +577,7 @@ int cmpc_export_qp(cmpc_handle h, int b, double *P_x, int32_t *P_i, int32_t *P_p
         P_p[n] = pp;
         for (int c = 0; c < n; ++c) q[c] = 0;
         for (int k = 0; k < K1; ++k)
-            for (int i = 0; i < 9; ++i) q[xi(k) + i] = st[(size_t)k * SS + 9 + i];
+            for (int i = 0; i < 9; ++i) q[xi(k) + i] = sf(k, 9 + i);
         for (int k = 0; k < K1; ++k) q[ti(k)] = 1.0;
         // ---- A rows in the reference order
         std::vector<std::tuple<int, int, double>> tr;   // (col, row, val)
@@ -597,7 +590,7 @@ int cmpc_export_qp(cmpc_handle h, int b, double *P_x, int32_t *P_i, int32_t *P_p
                 for (int j = 0; j < 9; ++j) add(xi(k) + j, A[(size_t)k * 81 + i * 9 + j]);
                 for (int j = 0; j < NU; ++j) add(ui(k) + j, Bm[(size_t)k * 9 * NU + i * NU + j]);
                 add(xi(k + 1) + i, -1.0);
-                const double r = st[(size_t)k * SS + i];
+                const double r = sf(k, i);
                 l[row] = r - 1e-12; u[row] = r + 1e-12;
             }
         for (int i = 0; i < 9; ++i, ++row) { add(xi(N) + i, 1.0); l[row] = u[row] = xb[(size_t)N * 9 + i]; }
@@ -617,16 +610,16 @@ int cmpc_export_qp(cmpc_handle h, int b, double *P_x, int32_t *P_i, int32_t *P_p
                 for (int r = 0; r < 5; ++r, ++row) {
                     l[row] = -inf; u[row] = 0;
                     if (lg[(size_t)k * NC + c] && r < 4) {
-                        const double *cs = &st[(size_t)k * SS + 32 + 32 * c];
-                        for (int qq = 0; qq < 3; ++qq) add(ui(k) + NUPC * c + FO + qq, cs[4 + 3 * r + qq]);
-                        u[row] = cs[16 + r];
+                        const int cs = 32 + 32 * c;
+                        for (int qq = 0; qq < 3; ++qq) add(ui(k) + NUPC * c + FO + qq, sf(k, cs + 4 + 3 * r + qq));
+                        u[row] = sf(k, cs + 16 + r);
                     }
                 }
         for (int k = 0; k < K1; ++k)
             for (int j = 0; j < 8; ++j, ++row) {
                 for (int i = 0; i < 3; ++i) add(xi(k) + 6 + i, ((j >> i) & 1) ? -1.0 : 1.0);
                 add(ti(k), cw);
-                l[row] = -inf; u[row] = st[(size_t)k * SS + 18 + j];
+                l[row] = -inf; u[row] = sf(k, 18 + j);
             }
         for (int k = 0; k < K1; ++k, ++row) { add(ti(k), -1.0); l[row] = -inf; u[row] = 0; }
         std::stable_sort(tr.begin(), tr.end(), [](auto &a, auto &c) {

@@ -86,6 +86,21 @@ template <typename T> struct DevBuf {
     T *Xacc, *Uacc, *Kacc, *Sacc;   // accepted solution (B,N+1,9) (B,N,NU) (B,N,108) (B,N+1,81)
 };
 
+// ---------------------------------------------------------------- knot-minor layouts
+// Per-knot records (stage records, IPM workspace) are stored field-major, knot-minor: field f
+// of knot k at p[f * KPC + k].  Thread k <-> knot k, so every field load or store of a wave is
+// one contiguous 512-B (fp64) access instead of 64 separate lines.  The pitch is a compile-time
+// constant covering every supported horizon (N + 2 <= 257 Schur blocks), so all field offsets
+// fold into immediates; the unused tail of each field row is never touched (no HBM traffic).
+constexpr int KPC = 264;
+
+// strided view of one knot's record: element i at p[i * KPC]
+template <typename T> struct SV {
+    T *p;
+    __device__ __forceinline__ T &operator[](int i) const { return p[i * KPC]; }
+    __device__ __forceinline__ SV operator+(int n) const { return SV{p + n * KPC}; }
+};
+
 // ---------------------------------------------------------------- small helpers
 template <typename T> __device__ __forceinline__ T sq(T a) { return a * a; }
 
@@ -137,7 +152,7 @@ __device__ __forceinline__ void block_reduce(T (&v)[NV], T *red) {
 }
 
 // skew(v) * x  == v cross x
-template <typename T> __device__ __forceinline__ void cross3(const T *a, const T *b, T *o) {
+template <typename A, typename B, typename T> __device__ __forceinline__ void cross3(const A &a, const B &b, T *o) {
     o[0] = a[1] * b[2] - a[2] * b[1];
     o[1] = a[2] * b[0] - a[0] * b[2];
     o[2] = a[0] * b[1] - a[1] * b[0];

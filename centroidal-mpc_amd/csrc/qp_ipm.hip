@@ -11,12 +11,23 @@
 // row).  Friction rows use the push-through form Phi^-1 G'D = W^-1 G'(D^-1 + G W^-1 G')^-1 so
 // no D * r product ever forms (D = lambda/s reaches 1e15+ near convergence).
 //
-// Mapping (one 256-thread workgroup per problem, all IPM iterations in one launch):
+// Mapping (one 128-thread workgroup per problem, all IPM iterations in one launch):
 //   thread k <-> knot k for every per-knot phase (residuals, Phi factors, S blocks, Newton
-//   back-substitution, step length); wave 0 runs the O(N) block-Cholesky of S and the two
-//   block sweeps per Newton solve with the 9x9 blocks staged in LDS.  Problems are
-//   independent, so the grid needs no inter-workgroup communication.
+//   back-substitution, step length); waves 0 and 1 run the two ends of the block factorization
+//   of S and of the two block sweeps per Newton solve.  Problems are independent, so the grid
+//   needs no inter-workgroup communication.
+// Layout: every per-knot workspace array and the stage records are field-major, knot-minor
+// (field f of knot k at base + f * KPC + k, common.hpp), so each field access of a wave is one
+// contiguous 512-B transaction; per-block vectors (nu, r_e) use the same scheme over the N + 2
+// Schur blocks.  The Schur right-hand side / direction dnu never leave LDS.
 #include "common.hpp"
+
+#ifdef CMPC_NOINLINE
+#define PHASE_ATTR __attribute__((noinline))
+#else
+#define PHASE_ATTR
+#endif
+#define WF(f) (Ws<ROBOT>::f)   // workspace field row
 
 namespace cmpc {
 
@@ -26,23 +37,21 @@ constexpr int FU = 34;   // per-contact factor record: Gw 12 | Kinv 10 | F 6 | W
 // 1/den | D_slack  (K_TR = D_TR^-1 + G_L W_L^-1 G_L', see phase_factor)
 constexpr int FX = 64, FX_ML = 6, FX_L = 12, FX_Z1 = 48, FX_DEN = 56, FX_DSL = 57;
 
-// Workspace offsets (elements) for one problem.
-struct WsLayout {
-    size_t s, l, x, u, t, nu, rdx, rdt, rdu, rde, rdi, facx, facu, Sd, So, wx, wt, wu, rhs, dnu, dx, dt, du,
-        ds, dl, dsa, dla, rh, total;
-    __host__ __device__ WsLayout(int N, int NI, int NC) {
-        const size_t K1 = N + 1, NB = N + 2;
-        size_t o = 0;
-        auto take = [&](size_t n) { size_t r = o; o += (n + 7) & ~size_t(7); return r; };
-        s = take(K1 * NI); l = take(K1 * NI); x = take(K1 * 9); u = take(N * NU); t = take(K1);
-        nu = take(NB * 9); rdx = take(K1 * 9); rdt = take(K1); rdu = take(N * NU); rde = take(NB * 9);
-        rdi = take(K1 * NI); facx = take(K1 * FX); facu = take((size_t)N * NC * FU); Sd = take(NB * 81);
-        So = take((N + 1) * 81); wx = take(K1 * 9); wt = take(K1); wu = take(N * NU); rhs = take(NB * 9);
-        dnu = take(NB * 9); dx = take(K1 * 9); dt = take(K1); du = take(N * NU); ds = take(K1 * NI);
-        dl = take(K1 * NI); dsa = take(K1 * NI); dla = take(K1 * NI);
-        rh = take(K1 * NI);
-        total = o;
-    }
+// Workspace of one problem.  Per-knot arrays and the per-block vectors (nu, r_e; block j in
+// column j) are field rows of pitch KPC (field-major, see the layout note above); their offsets
+// are compile-time constants.  The Schur blocks follow the field rows (see tw_factor_ends).
+constexpr int NBMAX = 257;   // Schur blocks at the largest supported horizon (N = 255)
+template <int ROBOT> struct Ws {
+    static constexpr int NI = Rows<ROBOT>::NI, NC = Robot<ROBOT>::NC;
+    enum : int {   // field rows
+        s = 0, l = s + NI, x = l + NI, u = x + 9, t = u + NU, nu = t + 1, rdx = nu + 9, rdt = rdx + 9,
+        rdu = rdt + 1, rde = rdu + NU, rdi = rde + 9, facx = rdi + NI, facu = facx + FX, wx = facu + NC * FU,
+        wt = wx + 9, wu = wt + 1, dx = wu + NU, dt = dx + 9, du = dt + 1, ds = du + NU, dl = ds + NI,
+        dsa = dl + NI, dla = dsa + NI, rh = dla + NI, NF = rh + NI
+    };
+    // Schur blocks (block-major 9x9): S_jj -> I_j, and S_{j,j+1} -> X_{j+1} / Y_j (tw_factor_ends)
+    static constexpr size_t Sd = (size_t)NF * KPC, So = Sd + (size_t)NBMAX * 81;
+    static constexpr size_t total = (So + (size_t)NBMAX * 81 + 7) & ~size_t(7);
 };
 
 template <typename T> __device__ __forceinline__ T rcp_nr(T p) {
@@ -64,26 +73,26 @@ template <typename T> __device__ __forceinline__ T tr_sign(int j, int i) { retur
 
 // ------------------------------------------------------------------ compact A, B operators
 // A = [[I, beta I, 0], [0, I, 0], [[w]x, 0, I]] in (c, l, L) blocks.
-template <typename T> __device__ __forceinline__ void opA(const T *w, T beta, const T *x, T *o) {
+template <typename T, typename W> __device__ __forceinline__ void opA(const W &w, T beta, const T *x, T *o) {
     for (int i = 0; i < 3; ++i) o[i] = x[i] + beta * x[3 + i];
     for (int i = 0; i < 3; ++i) o[3 + i] = x[3 + i];
     T wc[3];
     cross3(w, x, wc);
     for (int i = 0; i < 3; ++i) o[6 + i] = x[6 + i] + wc[i];
 }
-template <typename T> __device__ __forceinline__ void opAT(const T *w, T beta, const T *v, T *o) {
+template <typename T, typename W> __device__ __forceinline__ void opAT(const W &w, T beta, const T *v, T *o) {
     T vw[3];
     cross3(v + 6, w, vw);   // [w]x' v_L = v_L x w
     for (int i = 0; i < 3; ++i) o[i] = v[i] + vw[i];
     for (int i = 0; i < 3; ++i) o[3 + i] = beta * v[i] + v[3 + i];
     for (int i = 0; i < 3; ++i) o[6 + i] = v[6 + i];
 }
-template <typename T, int ROBOT> __device__ __forceinline__ void opB(const T *st, const T *u, T *o) {
+template <typename T, int ROBOT, typename SR> __device__ __forceinline__ void opB(const SR &st, const T *u, T *o) {
     constexpr int NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
     using S = Stage<ROBOT>;
     for (int i = 0; i < 9; ++i) o[i] = T(0);
     for (int c = 0; c < NC; ++c) {
-        const T *cs = st + S::CON + S::CS * c;
+        const auto cs = st + (S::CON + S::CS * c);
         const T a = cs[S::ALPHA];
         const T *f = u + NUPC * c + FO;
         T lf[3];
@@ -96,11 +105,11 @@ template <typename T, int ROBOT> __device__ __forceinline__ void opB(const T *st
         }
     }
 }
-template <typename T, int ROBOT> __device__ __forceinline__ void opBT(const T *st, const T *v, T *o) {
+template <typename T, int ROBOT, typename SR> __device__ __forceinline__ void opBT(const SR &st, const T *v, T *o) {
     constexpr int NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
     using S = Stage<ROBOT>;
     for (int c = 0; c < NC; ++c) {
-        const T *cs = st + S::CON + S::CS * c;
+        const auto cs = st + (S::CON + S::CS * c);
         const T a = cs[S::ALPHA];
         T vl[3];
         cross3(v + 6, cs + S::LEVER, vl);   // [lev]x' v_L = v_L x lev
@@ -125,17 +134,20 @@ template <typename T, int ROBOT> struct Ctx {
     using S = Stage<ROBOT>;
     int N;
     const DevParams<T> *prm;
-    const T *stage;       // (N+1, SIZE)
+    const T *stage;       // (SIZE, KPC) field-major
     const uint8_t *logic; // (N, NC)
     const T *xbar;        // (N+1, 9)
     T cw, beta;
     T *ws;
-    WsLayout L;
-    T *Sd, *So;           // Schur blocks: LDS-resident when they fit (SL), else workspace
+    T *Sd, *So;           // Schur diagonal blocks / inverses and couplings (workspace, see tw_factor_ends)
+    LdsT<T> *vb;          // Schur rhs -> direction dnu, (N+2) x 9 block vector in LDS
     T dcap;               // cap on D = lambda/s for the CoP rows (D-form, folded into W_cop)
     __device__ T Dform(T l, T s_) const { return fmin(fdiv(l, s_), dcap); }
 
-    __device__ const T *st(int k) const { return stage + (size_t)k * S::SIZE; }
+    __device__ SV<const T> st(int k) const { return SV<const T>{stage + k}; }
+    // per-knot record k / per-block vector j of workspace field row f (Ws<ROBOT>::...)
+    __device__ SV<T> kv(int f, int k) const { return SV<T>{ws + f * KPC + k}; }
+    __device__ SV<T> bv(int f, int j) const { return SV<T>{ws + f * KPC + j}; }
     // contact-active bits of knot k, loaded once per phase (0 at k = N: only the TR rows exist)
     __device__ unsigned cmask(int k) const {
         if (k >= N) return 0u;
@@ -165,7 +177,7 @@ template <typename T, int ROBOT> struct Ctx {
         if (row == 8) return -t;
         if (row < R_::CP) {
             const int c = (row - R_::FR) / 4, r = (row - R_::FR) % 4;
-            const T *cs = st(k) + S::CON + S::CS * c;
+            const auto cs = st(k) + (S::CON + S::CS * c);
             const T *f = u + NUPC * c + FO;
             T v = cs[S::G + 3 * r] * f[0] + cs[S::G + 3 * r + 1] * f[1] + cs[S::G + 3 * r + 2] * f[2];
             return with_h ? v - cs[S::H + r] : v;
@@ -190,7 +202,7 @@ template <typename T, int ROBOT> struct Ctx {
         if (k >= N) return;
         for (int i = 0; i < NU; ++i) gu[i] = T(0);
         for (int c = 0; c < NC; ++c) {   // rows of inactive contacts carry v = 0 and G = 0
-            const T *cs = st(k) + S::CON + S::CS * c;
+            const auto cs = st(k) + (S::CON + S::CS * c);
             for (int r = 0; r < 4; ++r) {
                 const T vr = v[R_::FR + 4 * c + r];
                 for (int q = 0; q < 3; ++q) gu[NUPC * c + FO + q] += cs[S::G + 3 * r + q] * vr;
@@ -201,8 +213,8 @@ template <typename T, int ROBOT> struct Ctx {
             }
         }
     }
-    __device__ T *var_x(int k) const { return ws + L.x + (size_t)k * 9; }
-    __device__ T *var_u(int k) const { return ws + L.u + (size_t)k * NU; }
+    __device__ SV<T> var_x(int k) const { return kv(Ws<ROBOT>::x, k); }
+    __device__ SV<T> var_u(int k) const { return kv(Ws<ROBOT>::u, k); }
 };
 
 // 3x3 symmetric packed (00,10,11,20,21,22) helpers
@@ -292,20 +304,22 @@ template <int n, typename T, typename P> __device__ __forceinline__ void stv(P p
     for (int i = 0; i < n; ++i) p[i] = v[i];
 }
 
-template <typename T, int ROBOT> __device__ void phase_residual(const Ctx<T, ROBOT> &C, int k, Norms<T, ROBOT> &nm) {
+template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_residual(const Ctx<T, ROBOT> &C, int k, Norms<T, ROBOT> &nm) {
     using S = Stage<ROBOT>;
     constexpr int NI = Rows<ROBOT>::NI;
     const int N = C.N;
     const bool hu = k < N;
     const DevParams<T> &P = *C.prm;
-    const T *nu = C.ws + C.L.nu;
-    const T *st = C.st(k);
-    T x[9], u[NU], sv[NI], lm[NI];
+    const auto st = C.st(k);
+    T x[9], u[NU], sv[NI], lm[NI], nk[9], n1[9], x1[9];
     ldv(C.var_x(k), x);
-    ldv(C.var_u(hu ? k : 0), u);   // k = N: no controls (values unused)
-    ldv(C.ws + C.L.s + (size_t)k * NI, sv);
-    ldv(C.ws + C.L.l + (size_t)k * NI, lm);
-    const T t = C.ws[C.L.t + k];
+    ldv(C.var_u(k), u);                  // k = N: padding column (values unused)
+    ldv(C.kv(WF(s), k), sv);
+    ldv(C.kv(WF(l), k), lm);
+    ldv(C.bv(WF(nu), k), nk);            // nu block k (k = 0: the initial-state rows)
+    ldv(C.bv(WF(nu), k + 1), n1);        // nu block k+1 (k = N: the final-state rows)
+    ldv(C.var_x(hu ? k + 1 : k), x1);
+    const T t = C.kv(WF(t), k)[0];
     const unsigned msk = C.cmask(k);
     T lv[NI];
 #pragma unroll
@@ -313,16 +327,15 @@ template <typename T, int ROBOT> __device__ void phase_residual(const Ctx<T, ROB
     T gL[3], gt, gu[NU];
     C.gtv(k, lv, gL, gt, gu);
     // E' nu at knot k
-    T ex[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, eu[NU];
-    if (k == 0) for (int i = 0; i < 9; ++i) ex[i] += nu[i];
+    T ex[9], eu[NU];
+    for (int i = 0; i < 9; ++i) ex[i] = (k == 0) ? nk[i] : -nk[i];
+    if (k == N) for (int i = 0; i < 9; ++i) ex[i] += n1[i];
     if (hu) {
         T a[9];
-        opAT(st + S::W, C.beta, nu + (size_t)(1 + k) * 9, a);
+        opAT(st + S::W, C.beta, n1, a);
         for (int i = 0; i < 9; ++i) ex[i] += a[i];
-        opBT<T, ROBOT>(st, nu + (size_t)(1 + k) * 9, eu);
+        opBT<T, ROBOT>(st, n1, eu);
     }
-    if (k >= 1) for (int i = 0; i < 9; ++i) ex[i] -= nu[(size_t)k * 9 + i];
-    if (k == N) for (int i = 0; i < 9; ++i) ex[i] += nu[(size_t)(N + 1) * 9 + i];
     T rdx[9];
     for (int i = 0; i < 9; ++i) {
         const T hx = P.Wx[i] * x[i], q = st[S::QX + i];
@@ -343,8 +356,7 @@ template <typename T, int ROBOT> __device__ void phase_residual(const Ctx<T, ROB
             nm.sd = fmax(nm.sd, fmax(fabs(h), fmax(fabs(eu[i]), fabs(gu[i]))));
         }
         // dynamics row block 1+k
-        T ax[9], bu[9], x1[9];
-        ldv(C.var_x(k + 1), x1);
+        T ax[9], bu[9];
         opA(st + S::W, C.beta, x, ax);
         opB<T, ROBOT>(st, u, bu);
         for (int i = 0; i < 9; ++i) {
@@ -379,25 +391,35 @@ template <typename T, int ROBOT> __device__ void phase_residual(const Ctx<T, ROB
         nm.lmax = fmax(nm.lmax, pr ? lm[r] : T(0));
     }
     // stores
-    stv(C.ws + C.L.rdx + (size_t)k * 9, rdx);
-    C.ws[C.L.rdt + k] = rdt;
+    stv(C.kv(WF(rdx), k), rdx);
+    C.kv(WF(rdt), k)[0] = rdt;
     if (hu) {
-        stv(C.ws + C.L.rdu + (size_t)k * NU, rdu);
-        stv(C.ws + C.L.rde + (size_t)(1 + k) * 9, rde);
+        stv(C.kv(WF(rdu), k), rdu);
+        stv(C.bv(WF(rde), 1 + k), rde);
     }
-    if (bnd) stv(C.ws + C.L.rde + (size_t)(k == 0 ? 0 : N + 1) * 9, rdb);
-    stv(C.ws + C.L.rdi + (size_t)k * NI, rdi);
+    if (bnd) stv(C.bv(WF(rde), k == 0 ? 0 : N + 1), rdb);
+    stv(C.kv(WF(rdi), k), rdi);
 }
 
 // (2) Phi factors of knot k
-template <typename T, int ROBOT> __device__ void phase_factor(const Ctx<T, ROBOT> &C, int k) {
+template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_factor(const Ctx<T, ROBOT> &C, int k) {
     using S = Stage<ROBOT>;
     using R_ = Rows<ROBOT>;
     constexpr int NI = R_::NI, NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
     const int N = C.N;
     const DevParams<T> &P = *C.prm;
-    const T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
-    T *fx = C.ws + C.L.facx + (size_t)k * FX;
+    T s[NI], lm[NI];
+    ldv(C.kv(WF(s), k), s);
+    ldv(C.kv(WF(l), k), lm);
+    const unsigned msk = C.cmask(k);
+    // friction rows of every contact, loaded before the first factor store
+    T Gr[NC][12];
+    {
+        const auto st = C.st(k < N ? k : 0);
+        for (int c = 0; c < NC; ++c)
+            for (int e = 0; e < 12; ++e) Gr[c][e] = st[S::CON + S::CS * c + S::G + e];
+    }
+    const SV<T> fx = C.kv(WF(facx), k);
     // (L, t) block in push-through form (no D * r product, no cancellation as rows pin L or t):
     //   K = D_TR^-1 + Y G_L' (8x8 SPD; Y = G_L W_L^-1; D^-1 floored: at a vertex of the trust
     //   region more than 3 rows are active and K -> rank 3),  L L' = K,  z1 = L^-1 1,
@@ -447,33 +469,33 @@ template <typename T, int ROBOT> __device__ void phase_factor(const Ctx<T, ROBOT
     fx[FX_DSL] = dsl;
     if (k >= N) return;
     for (int c = 0; c < NC; ++c) {
-        T *fu = C.ws + C.L.facu + ((size_t)k * NC + c) * FU;
+        const SV<T> fu = C.kv(WF(facu), k) + c * FU;
         const T *Wc = P.Wu + NUPC * c;
+        const bool act = (msk >> c) & 1u;
         // Winvd: inverse diagonal of W' (CoP rows fold into their coordinate's diagonal)
         for (int q = 0; q < NUPC; ++q) fu[28 + q] = T(1) / Wc[q];
-        if (ROBOT == 1 && C.logic[k * NC + c]) {
+        if (ROBOT == 1 && act) {
             for (int dd = 0; dd < 2; ++dd) {
                 const int r0 = R_::CP + 4 * c + 2 * dd;
                 fu[28 + dd] = T(1) / (Wc[dd] + C.Dform(lm[r0], s[r0]) + C.Dform(lm[r0 + 1], s[r0 + 1]));
             }
         }
         const T wi[3] = {T(1) / Wc[FO], T(1) / Wc[FO + 1], T(1) / Wc[FO + 2]};
-        if (!C.logic[k * NC + c]) {
+        if (!act) {
             for (int q = 0; q < 12; ++q) fu[q] = T(0);
             for (int q = 0; q < 10; ++q) fu[12 + q] = T(0);
             fu[12 + 0] = fu[12 + 2] = fu[12 + 5] = fu[12 + 9] = T(1);
             fu[22] = wi[0]; fu[23] = T(0); fu[24] = wi[1]; fu[25] = T(0); fu[26] = T(0); fu[27] = wi[2];
             continue;
         }
-        const T *cs = C.st(k) + S::CON + S::CS * c;
         T Gw[4][3];
         for (int r = 0; r < 4; ++r)
-            for (int q = 0; q < 3; ++q) { Gw[r][q] = cs[S::G + 3 * r + q] * wi[q]; fu[3 * r + q] = Gw[r][q]; }
+            for (int q = 0; q < 3; ++q) { Gw[r][q] = Gr[c][3 * r + q] * wi[q]; fu[3 * r + q] = Gw[r][q]; }
         T Km[4][4], tr = T(0);
         for (int r = 0; r < 4; ++r)
             for (int q = 0; q < 4; ++q) {
                 T acc = T(0);
-                for (int z = 0; z < 3; ++z) acc += Gw[r][z] * cs[S::G + 3 * q + z];
+                for (int z = 0; z < 3; ++z) acc += Gw[r][z] * Gr[c][3 * q + z];
                 Km[r][q] = acc;
             }
         for (int r = 0; r < 4; ++r) tr += Km[r][r];
@@ -499,12 +521,14 @@ template <typename T, int ROBOT> __device__ void phase_factor(const Ctx<T, ROBOT
 template <typename T, int ROBOT> __device__ void phi_solve_u(const Ctx<T, ROBOT> &C, int k, const T *vu, T *ou) {
     constexpr int NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
     for (int c = 0; c < NC; ++c) {
-        const T *fu = C.ws + C.L.facu + ((size_t)k * NC + c) * FU;
+        const SV<T> fu = C.kv(WF(facu), k) + c * FU;
         const T *vc = vu + NUPC * c;
         T *oc = ou + NUPC * c;
         for (int q = 0; q < NUPC; ++q) oc[q] = fu[28 + q] * vc[q];
+        T F[6];
+        ldv(fu + 22, F);
         for (int i = 0; i < 3; ++i)
-            oc[FO + i] = sym3(fu + 22, i, 0) * vc[FO] + sym3(fu + 22, i, 1) * vc[FO + 1] + sym3(fu + 22, i, 2) * vc[FO + 2];
+            oc[FO + i] = sym3(F, i, 0) * vc[FO] + sym3(F, i, 1) * vc[FO + 1] + sym3(F, i, 2) * vc[FO + 2];
     }
 }
 
@@ -515,8 +539,11 @@ template <typename T, int ROBOT> __device__ void phi_solve_u(const Ctx<T, ROBOT>
 // dL = W_L^-1 (vL - G_L' dlam);  dlam_sl = cw 1'dlam - vt  (the t row of the dual residual)
 template <typename T, int ROBOT>
 __device__ void tr_local(const Ctx<T, ROBOT> &C, int k, const T *vL, T vt, const T *rh, T *dL, T &dt, T *dlt, T &dls) {
-    const T *fx = C.ws + C.L.facx + (size_t)k * FX;
-    const T *Lk = fx + FX_L, *z1 = fx + FX_Z1;
+    const SV<T> fx = C.kv(WF(facx), k);
+    T Lk[36], z1[8];
+    ldv(fx + FX_L, Lk);
+    ldv(fx + FX_Z1, z1);
+    const T fdsl = fx[FX_DSL], fden = fx[FX_DEN];
     const T wl[3] = {rcp_nr(C.prm->Wx[6]), rcp_nr(C.prm->Wx[7]), rcp_nr(C.prm->Wx[8])};
     T y[8];
     for (int j = 0; j < 8; ++j) {
@@ -527,7 +554,7 @@ __device__ void tr_local(const Ctx<T, ROBOT> &C, int k, const T *vL, T vt, const
     }
     T zy = T(0);
     for (int j = 0; j < 8; ++j) zy += z1[j] * y[j];
-    dt = (vt + fx[FX_DSL] * rh[8] - C.cw * zy) * fx[FX_DEN];
+    dt = (vt + fdsl * rh[8] - C.cw * zy) * fden;
     for (int j = 0; j < 8; ++j) y[j] += C.cw * dt * z1[j];
     for (int j = 7; j >= 0; --j) {
         T v = y[j];
@@ -545,19 +572,43 @@ __device__ void tr_local(const Ctx<T, ROBOT> &C, int k, const T *vL, T vt, const
 }
 
 // (3) S blocks owned by knot k
-template <typename T, int ROBOT> __device__ void phase_sblock(const Ctx<T, ROBOT> &C, int k) {
+template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_sblock(const Ctx<T, ROBOT> &C, int k) {
     using S = Stage<ROBOT>;
     constexpr int NC = Robot<ROBOT>::NC;
     const int N = C.N;
     const T beta = C.beta;
-    const T *fx = C.ws + C.L.facx + (size_t)k * FX;
+    const bool hu = k < N;
+    // loads: M_k, M_{k+1} (1/Wx[0:6] | M_LL packed), the stage's A/B data, the contacts' F, W'^-1
+    T f0[12], f1[12];
+    ldv(C.kv(WF(facx), k), f0);
+    ldv(C.kv(WF(facx), hu ? k + 1 : k), f1);
+    const auto st = C.st(k);
+    T w[3], w1[3];
+    ldv(st + S::W, w);
+    ldv(C.st(k + 1 < N ? k + 1 : k) + S::W, w1);
+    T al[NC], lev[NC][3], F[NC][6], wd[NC][6];
+    for (int c = 0; c < NC; ++c) {
+        const auto cs = st + (S::CON + S::CS * c);
+        al[c] = hu ? cs[S::ALPHA] : T(0);
+        ldv(cs + S::LEVER, lev[c]);
+        const SV<T> fu = C.kv(WF(facu), k) + c * FU;
+        ldv(fu + 22, F[c]);
+        ldv(fu + 28, wd[c]);
+    }
+    T bc[NC][6], bt[NC][3];
+    if (ROBOT == 1)
+        for (int c = 0; c < NC; ++c) {
+            const auto cs = st + (S::CON + S::CS * c);
+            ldv(cs + S::BCOP, bc[c]);
+            ldv(cs + S::BTAU, bt[c]);
+        }
     auto Mfull = [&](const T *f, int i, int j) -> T {   // M_k entry
         if (i < 6 || j < 6) return (i == j && i < 6) ? f[i] : T(0);
         return sym3(f + 6, i - 6, j - 6);
     };
     // M A' blocks:  [[Mc, 0, Mc W'], [beta Ml, Ml, 0], [0, 0, ML]]
-    auto MAt = [&](const T *f, const T *w, int i, int j) -> T {
-        const T Wm[3][3] = {{0, -w[2], w[1]}, {w[2], 0, -w[0]}, {-w[1], w[0], 0}};
+    auto MAt = [&](const T *f, const T *wv, int i, int j) -> T {
+        const T Wm[3][3] = {{0, -wv[2], wv[1]}, {wv[2], 0, -wv[0]}, {-wv[1], wv[0], 0}};
         if (i < 3) {
             if (j < 3) return (i == j) ? f[i] : T(0);
             if (j < 6) return T(0);
@@ -575,24 +626,22 @@ template <typename T, int ROBOT> __device__ void phase_sblock(const Ctx<T, ROBOT
         T *Sd = C.Sd, *So = C.So;
         for (int i = 0; i < 9; ++i)
             for (int j = 0; j < 9; ++j) {
-                Sd[i * 9 + j] = Mfull(fx, i, j);
-                So[i * 9 + j] = MAt(fx, C.st(0) + S::W, i, j);
+                Sd[i * 9 + j] = Mfull(f0, i, j);
+                So[i * 9 + j] = MAt(f0, w, i, j);
             }
     }
     if (k == N) {
         T *Sd = C.Sd + (size_t)(N + 1) * 81;
         for (int i = 0; i < 9; ++i)
-            for (int j = 0; j < 9; ++j) Sd[i * 9 + j] = Mfull(fx, i, j);
+            for (int j = 0; j < 9; ++j) Sd[i * 9 + j] = Mfull(f0, i, j);
         return;
     }
-    const T *fx1 = fx + FX;
-    const T *w = C.st(k) + S::W;
     const T Wm[3][3] = {{0, -w[2], w[1]}, {w[2], 0, -w[0]}, {-w[1], w[0], 0}};
     T Sm[9][9];
     // A M A'
     for (int i = 0; i < 9; ++i)
         for (int j = 0; j < 9; ++j) Sm[i][j] = T(0);
-    const T *mc = fx, *ml = fx + 3;
+    const T *mc = f0, *ml = f0 + 3;
     for (int a = 0; a < 3; ++a) {
         Sm[a][a] = mc[a] + beta * beta * ml[a];
         Sm[a][3 + a] = Sm[3 + a][a] = beta * ml[a];
@@ -602,27 +651,23 @@ template <typename T, int ROBOT> __device__ void phase_sblock(const Ctx<T, ROBOT
         for (int bb = 0; bb < 3; ++bb) {
             Sm[a][6 + bb] = mc[a] * Wm[bb][a];   // Mc W'
             Sm[6 + bb][a] = Sm[a][6 + bb];
-            T acc = sym3(fx + 6, a, bb);
+            T acc = sym3(f0 + 6, a, bb);
             for (int q = 0; q < 3; ++q) acc += Wm[a][q] * mc[q] * Wm[bb][q];
             Sm[6 + a][6 + bb] = acc;
         }
-    // B Phi_u^-1 B'
+    // B Phi_u^-1 B'  (inactive contacts: alpha = 0)
     for (int c = 0; c < NC; ++c) {
-        const T *cs = C.st(k) + S::CON + S::CS * c;
-        const T al = cs[S::ALPHA];
-        if (al == T(0)) continue;
-        const T *fu = C.ws + C.L.facu + ((size_t)k * NC + c) * FU;
-        const T *lv = cs + S::LEVER;
+        const T *lv = lev[c];
         const T Lm[3][3] = {{0, -lv[2], lv[1]}, {lv[2], 0, -lv[0]}, {-lv[1], lv[0], 0}};
-        T F[3][3], FL[3][3];   // F, F Lambda'
+        T Fm[3][3], FL[3][3];   // F, F Lambda'
         for (int i = 0; i < 3; ++i)
-            for (int j = 0; j < 3; ++j) F[i][j] = sym3(fu + 22, i, j);
+            for (int j = 0; j < 3; ++j) Fm[i][j] = sym3(F[c], i, j);
         for (int i = 0; i < 3; ++i)
-            for (int j = 0; j < 3; ++j) FL[i][j] = F[i][0] * Lm[j][0] + F[i][1] * Lm[j][1] + F[i][2] * Lm[j][2];
-        const T a2 = al * al;
+            for (int j = 0; j < 3; ++j) FL[i][j] = Fm[i][0] * Lm[j][0] + Fm[i][1] * Lm[j][1] + Fm[i][2] * Lm[j][2];
+        const T a2 = al[c] * al[c];
         for (int i = 0; i < 3; ++i)
             for (int j = 0; j < 3; ++j) {
-                Sm[3 + i][3 + j] += a2 * F[i][j];
+                Sm[3 + i][3 + j] += a2 * Fm[i][j];
                 Sm[3 + i][6 + j] += a2 * FL[i][j];
                 Sm[6 + j][3 + i] += a2 * FL[i][j];
                 T acc = T(0);
@@ -630,29 +675,28 @@ template <typename T, int ROBOT> __device__ void phase_sblock(const Ctx<T, ROBOT
                 Sm[6 + i][6 + j] += a2 * acc;
             }
         if (ROBOT == 1) {
-            const T *bc = cs + S::BCOP, *bt = cs + S::BTAU;
+            const T on = al[c] != T(0) ? T(1) : T(0);
             for (int i = 0; i < 3; ++i)
                 for (int j = 0; j < 3; ++j)
-                    Sm[6 + i][6 + j] += bc[2 * i] * fu[28] * bc[2 * j] + bc[2 * i + 1] * fu[29] * bc[2 * j + 1] +
-                                        bt[i] * fu[33] * bt[j];
+                    Sm[6 + i][6 + j] += on * (bc[c][2 * i] * wd[c][0] * bc[c][2 * j] +
+                                              bc[c][2 * i + 1] * wd[c][1] * bc[c][2 * j + 1] +
+                                              bt[c][i] * wd[c][5] * bt[c][j]);
         }
     }
     // + M_{k+1}
     for (int i = 0; i < 9; ++i)
-        for (int j = 0; j < 9; ++j) Sm[i][j] += Mfull(fx1, i, j);
+        for (int j = 0; j < 9; ++j) Sm[i][j] += Mfull(f1, i, j);
     T *Sd = C.Sd + (size_t)(1 + k) * 81;
     for (int e = 0; e < 81; ++e) Sd[e] = Sm[e / 9][e % 9];
     T *So = C.So + (size_t)(1 + k) * 81;
     if (k + 1 < N) {
-        const T *w1 = C.st(k + 1) + S::W;
         for (int i = 0; i < 9; ++i)
-            for (int j = 0; j < 9; ++j) So[i * 9 + j] = -MAt(fx1, w1, i, j);
+            for (int j = 0; j < 9; ++j) So[i * 9 + j] = -MAt(f1, w1, i, j);
     } else {
         for (int i = 0; i < 9; ++i)
-            for (int j = 0; j < 9; ++j) So[i * 9 + j] = -Mfull(fx1, i, j);
+            for (int j = 0; j < 9; ++j) So[i * 9 + j] = -Mfull(f1, i, j);
     }
 }
-
 
 // (4) two-ended ("twisted") block-Thomas factorization of the SPD block-tridiagonal S with
 // explicit symmetric inverses.  Wave 0 eliminates from the top, wave 1 from the bottom, and the
@@ -660,23 +704,28 @@ template <typename T, int ROBOT> __device__ void phase_sblock(const Ctx<T, ROBOT
 //   top    (j < m):  X_j = S_{j,j-1} I_{j-1},  I_j = (S_jj - X_j S_{j-1,j})^-1      So[j-1] <- X_j
 //   bottom (j > m):  Y_j = S_{j,j+1} I_{j+1},  I_j = (S_jj - Y_j S_{j+1,j})^-1      So[j]   <- Y_j
 //   meet   (j = m):  I_m = (S_mm - X_m S_{m-1,m} - Y_m S_{m+1,m})^-1
-// Sd[j] <- I_j (LDS when it fits: the inverses are re-read by every sweep); So[j] holds
-// S_{j,j+1} on input and lives in global memory: each step stages the raw block it needs into
-// LDS scratch from registers loaded one step ahead.  Inverses by Gauss-Jordan sweeps over the
-// 64 lanes (SPD: no pivoting) with a pivot floor relative to the original diagonal (near the
-// solution of a degenerate QP the Schur blocks are differences of O(M) numbers).
-template <typename T, typename PS>
-__device__ __forceinline__ void tw_step(PS *Sd, const LdsT<T> *Op, const LdsT<T> *Oq, T *OwTop, T *OwBot, int j,
-                                        LdsT<T> *A, LdsT<T> *Xb) {
+// Sd[j] holds S_jj on input and I_j on output, So[j] holds S_{j,j+1} on input (both in the
+// workspace, so the kernel's LDS stays small and several problems share a CU).  Each wave keeps
+// its previous inverse and the step's blocks in a small LDS scratch; the next step's raw blocks
+// are fetched one step ahead (a step is thousands of cycles).  Inverses by Gauss-Jordan sweeps
+// over the 64 lanes (SPD: no pivoting) with a pivot floor relative to the original diagonal
+// (near the solution of a degenerate QP the Schur blocks are differences of O(M) numbers).
+// Per-wave LDS scratch: A (current) | P (previous inverse) | Xb | Ob | Dd (original diagonal).
+constexpr int TW_SCRATCH = 4 * 88 + 16;
+
+template <typename T>
+__device__ __forceinline__ void tw_step(T d0, T d1, const LdsT<T> *Op, const LdsT<T> *Ip, const LdsT<T> *Oq,
+                                        const LdsT<T> *Iq, T *Xout, T *Yout, T *Iout, LdsT<T> *A, LdsT<T> *P,
+                                        LdsT<T> *Xb, LdsT<T> *Dd) {
     const int lane = threadIdx.x & 63;
     const int e0 = lane, e1 = lane + 64;
     const bool has1 = e1 < 81;
     const int i0 = e0 / 9, c0 = e0 % 9, i1 = e1 / 9, c1 = e1 % 9;
-    PS *Dj = Sd + (size_t)j * 81;
-    T a0 = Dj[e0], a1 = has1 ? Dj[e1] : T(0);
+    T a0 = d0, a1 = d1;
+    if (e0 % 10 == 0) Dd[e0 / 10] = d0;
+    if (e1 == 80) Dd[8] = d1;
     T x0 = T(0), x1 = T(0), y0 = T(0), y1 = T(0);
     if (Op) {   // X = Op' I_{j-1};  A -= X Op   (Op = S_{j-1,j})
-        const PS *Ip = Sd + (size_t)(j - 1) * 81;
         for (int m = 0; m < 9; ++m) {
             x0 = fma(Op[m * 9 + i0], Ip[m * 9 + c0], x0);
             if (has1) x1 = fma(Op[m * 9 + i1], Ip[m * 9 + c1], x1);
@@ -691,7 +740,6 @@ __device__ __forceinline__ void tw_step(PS *Sd, const LdsT<T> *Op, const LdsT<T>
         wave_sync();
     }
     if (Oq) {   // Y = Oq I_{j+1};  A -= Y Oq'   (Oq = S_{j,j+1})
-        const PS *Iq = Sd + (size_t)(j + 1) * 81;
         for (int m = 0; m < 9; ++m) {
             y0 = fma(Oq[i0 * 9 + m], Iq[m * 9 + c0], y0);
             if (has1) y1 = fma(Oq[i1 * 9 + m], Iq[m * 9 + c1], y1);
@@ -707,11 +755,11 @@ __device__ __forceinline__ void tw_step(PS *Sd, const LdsT<T> *Op, const LdsT<T>
     }
     A[e0] = a0;
     if (has1) A[e1] = a1;
-    if (Op) { OwTop[e0] = x0; if (has1) OwTop[e1] = x1; }
-    if (Oq) { OwBot[e0] = y0; if (has1) OwBot[e1] = y1; }
+    if (Op) { Xout[e0] = x0; if (has1) Xout[e1] = x1; }
+    if (Oq) { Yout[e0] = y0; if (has1) Yout[e1] = y1; }
     wave_sync();
     for (int c = 0; c < 9; ++c) {
-        const T p = fmax(A[c * 9 + c], T(1e-13) * Dj[c * 9 + c]);
+        const T p = fmax(A[c * 9 + c], T(1e-13) * Dd[c]);
         const T ip = rcp_nr(p);
         const T aic0 = A[i0 * 9 + c], acj0 = A[c * 9 + c0], aij0 = A[e0];
         T aic1 = T(0), acj1 = T(0), aij1 = T(0);
@@ -727,191 +775,229 @@ __device__ __forceinline__ void tw_step(PS *Sd, const LdsT<T> *Op, const LdsT<T>
         if (has1) A[e1] = upd(i1, c1, aic1, acj1, aij1);
         wave_sync();
     }
-    Dj[e0] = A[e0];
-    if (has1) Dj[e1] = A[e1];
+    const T r0 = A[e0], r1 = has1 ? A[e1] : T(0);
+    P[e0] = r0;
+    if (has1) P[e1] = r1;
+    Iout[e0] = r0;
+    if (has1) Iout[e1] = r1;
     wave_sync();
 }
 
-// per-wave LDS scratch of the factorization: A | Xb | Ob (96 each)
-constexpr int TW_SCRATCH = 288;
-
 // the two ends (threads 0..127: wave 0 top blocks 0..m-1, wave 1 bottom blocks NB-1..m+1)
-template <typename T, typename PS> __device__ void tw_factor_ends(PS *Sd, T *So, int NB, int m, LdsT<T> *sh) {
+template <typename T> __device__ void tw_factor_ends(T *Sd, T *So, int NB, int m, LdsT<T> *sh) {
     const int lane = threadIdx.x & 63;
     const int e0 = lane, e1 = lane + 64;
     const bool has1 = e1 < 81;
     const bool top = (threadIdx.x >> 6) == 0;
-    LdsT<T> *A = sh + (top ? 0 : TW_SCRATCH), *Xb = A + 96, *Ob = A + 192;
-    T p0 = T(0), p1 = T(0);
-    auto fetch = [&](int blk) { p0 = So[(size_t)blk * 81 + e0]; p1 = has1 ? So[(size_t)blk * 81 + e1] : T(0); };
-    if (top) {
-        if (m > 1) fetch(0);
-        tw_step<T, PS>(Sd, nullptr, nullptr, nullptr, nullptr, 0, A, Xb);
-        for (int j = 1; j < m; ++j) {
-            Ob[e0] = p0;
-            if (has1) Ob[e1] = p1;
-            wave_sync();
-            if (j + 1 < m) fetch(j);
-            tw_step<T, PS>(Sd, Ob, nullptr, So + (size_t)(j - 1) * 81, nullptr, j, A, Xb);
+    LdsT<T> *A = sh + (top ? 0 : TW_SCRATCH), *P = A + 88, *Xb = A + 176, *Ob = A + 264, *Dd = A + 352;
+    T p0 = T(0), p1 = T(0), d0, d1, n0 = T(0), n1 = T(0);
+    auto fetch = [&](const T *blk, T &v0, T &v1) { v0 = blk[e0]; v1 = blk[has1 ? e1 : 80]; };
+    const int j0 = top ? 0 : NB - 1, dj = top ? 1 : -1, nstep = top ? m : NB - 1 - m;
+    fetch(Sd + (size_t)j0 * 81, d0, d1);
+    if (nstep > 1) {
+        fetch(So + (size_t)(top ? 0 : NB - 2) * 81, p0, p1);
+        fetch(Sd + (size_t)(j0 + dj) * 81, n0, n1);
+    }
+    tw_step<T>(d0, d1, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, Sd + (size_t)j0 * 81, A, P, Xb, Dd);
+    for (int s = 1, j = j0 + dj; s < nstep; ++s, j += dj) {
+        Ob[e0] = p0;
+        if (has1) Ob[e1] = p1;
+        d0 = n0;
+        d1 = n1;
+        wave_sync();
+        if (s + 1 < nstep) {   // raw blocks of the next step
+            fetch(So + (size_t)(top ? j : j - 1) * 81, p0, p1);
+            fetch(Sd + (size_t)(j + dj) * 81, n0, n1);
         }
-    } else {
-        if (NB - 2 > m) fetch(NB - 2);
-        tw_step<T, PS>(Sd, nullptr, nullptr, nullptr, nullptr, NB - 1, A, Xb);
-        for (int j = NB - 2; j > m; --j) {
-            Ob[e0] = p0;
-            if (has1) Ob[e1] = p1;
-            wave_sync();
-            if (j - 1 > m) fetch(j - 1);
-            tw_step<T, PS>(Sd, nullptr, Ob, nullptr, So + (size_t)j * 81, j, A, Xb);
-        }
+        if (top)
+            tw_step<T>(d0, d1, Ob, P, nullptr, nullptr, So + (size_t)(j - 1) * 81, nullptr, Sd + (size_t)j * 81, A,
+                       P, Xb, Dd);
+        else
+            tw_step<T>(d0, d1, nullptr, nullptr, Ob, P, nullptr, So + (size_t)j * 81, Sd + (size_t)j * 81, A, P,
+                       Xb, Dd);
     }
 }
 
-// the meeting block (wave 0, after a workgroup barrier)
-template <typename T, typename PS> __device__ void tw_factor_meet(PS *Sd, T *So, int m, LdsT<T> *sh) {
+// the meeting block (wave 0, after a workgroup barrier): I_{m-1} and I_{m+1} are the two waves'
+// previous inverses in LDS
+template <typename T> __device__ void tw_factor_meet(T *Sd, T *So, int m, LdsT<T> *sh) {
     const int lane = threadIdx.x & 63;
     const int e0 = lane, e1 = lane + 64;
     const bool has1 = e1 < 81;
-    LdsT<T> *A = sh, *Xb = A + 96, *Op = A + 192, *Oq = sh + TW_SCRATCH + 192;
+    LdsT<T> *A = sh, *P = A + 88, *Xb = A + 176, *Op = A + 264, *Dd = A + 352;
+    LdsT<T> *Pq = sh + TW_SCRATCH + 88, *Oq = sh + TW_SCRATCH + 264;
     Op[e0] = So[(size_t)(m - 1) * 81 + e0];
     Oq[e0] = So[(size_t)m * 81 + e0];
     if (has1) { Op[e1] = So[(size_t)(m - 1) * 81 + e1]; Oq[e1] = So[(size_t)m * 81 + e1]; }
+    const T d0 = Sd[(size_t)m * 81 + e0], d1 = has1 ? Sd[(size_t)m * 81 + e1] : T(0);
     wave_sync();
-    tw_step<T, PS>(Sd, Op, Oq, So + (size_t)(m - 1) * 81, So + (size_t)m * 81, m, A, Xb);
+    tw_step<T>(d0, d1, Op, P, Oq, Pq, So + (size_t)(m - 1) * 81, So + (size_t)m * 81, Sd + (size_t)m * 81, A, P,
+               Xb, Dd);
 }
 
-// (5c) two-ended block sweeps with the twisted factors: rhs -> dnu (vector staged in LDS vb)
+// Chunked, double-buffered stream of 9x9 blocks from the workspace into per-wave LDS: each sweep
+// iteration issues the next K blocks (two elements per lane, coalesced), runs K sweep steps out of
+// the current LDS chunk, then lands the next chunk, so one chunk's L2 / Infinity-Cache latency
+// hides behind K dependent steps.  Loads, their landing and their use stay inside one loop
+// iteration (no in-flight registers carried over the back-edge, where the compiler's wait
+// counting would drain the queue), and the loads are branch-free (a clamped index past the end
+// re-reads the last block).
+constexpr int RSLOT = 88;
+template <typename T, int K> struct ChunkStream {
+    const T *base;   // block i at base + i * step
+    long step;
+    int n;
+    LdsT<T> *buf;    // 2 x K slots of RSLOT
+    T r0[K], r1[K];
+    __device__ __forceinline__ void issue(int c) {
+        const int lane = threadIdx.x & 63;
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            const int i = c * K + q;
+            const T *p = base + (i < n ? i : n - 1) * step;
+            r0[q] = p[lane];
+            r1[q] = p[lane + 64 < 81 ? lane + 64 : 80];
+        }
+    }
+    __device__ __forceinline__ void land(int c) {
+        const int lane = threadIdx.x & 63;
+        LdsT<T> *b = buf + (c & 1) * K * RSLOT;
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            b[q * RSLOT + lane] = r0[q];
+            if (lane + 64 < 81) b[q * RSLOT + lane + 64] = r1[q];
+        }
+    }
+    __device__ __forceinline__ const LdsT<T> *blk(int i) const {
+        return buf + ((i / K) & 1) * K * RSLOT + (i % K) * RSLOT;
+    }
+};
+constexpr int KE = 8, KB = 4;   // chunk sizes of the elimination (one stream) and back (two) sweeps
+constexpr int SWEEP_LDS = 2 * KE * RSLOT;   // per wave: 2 x 8 slots = 2 x (2 x 4) slots
+
+// (5c) two-ended block sweeps with the twisted factors: rhs -> dnu in place in the LDS vector vb
 //   top:    y_0 = b_0, y_j = b_j - X_j y_{j-1}           bottom: y_j = b_j - Y_j y_{j+1}
 //   meet:   x_m = I_m (b_m - X_m y_{m-1} - Y_m y_{m+1})
 //   up:     x_j = I_j y_j - X_{j+1}' x_{j+1}  (j < m)   down: x_j = I_j y_j - Y_{j-1}' x_{j-1}  (j > m)
-// X_j sits at So[j-1], Y_j at So[j] (global; lane r < 9 reads its row / column one step ahead).
-// Three stages separated by workgroup barriers.
-template <typename T> __device__ __forceinline__ void ld_row(const T *p, T (&r)[9]) {
-    for (int q = 0; q < 9; ++q) r[q] = p[q];
-}
-template <typename T> __device__ __forceinline__ void ld_col(const T *p, T (&r)[9]) {
-    for (int q = 0; q < 9; ++q) r[q] = p[q * 9];
-}
-
-template <typename T> __device__ void tw_solve_elim(const T *Xs, const T *rhs, int NB, int m, LdsT<T> *vb) {
+// X_j sits at So[j-1], Y_j at So[j].  Three stages separated by workgroup barriers.
+template <typename T> __device__ void tw_solve_elim(const T *Xs, int NB, int m, LdsT<T> *vb, LdsT<T> *ring) {
     const int lane = threadIdx.x & 63;
     const bool top = (threadIdx.x >> 6) == 0;
     const int lr = lane < 9 ? lane : 0;
-    const int lo = top ? 0 : m + 1, hi = top ? m + 1 : NB;   // rhs blocks staged by this wave
-    for (int e = lo * 9 + lane; e < hi * 9; e += WAVE) vb[e] = rhs[e];
-    wave_sync();
-    T nx[9], cur[9];
-    if (top) {
-        if (m > 1) ld_row(Xs + lr * 9, nx);                             // X_1 at So[0]
-        for (int j = 1; j < m; ++j) {
-            for (int q = 0; q < 9; ++q) cur[q] = nx[q];
-            if (j + 1 < m) ld_row(Xs + (size_t)j * 81 + lr * 9, nx);     // X_{j+1} at So[j]
+    // step i: top j = i + 1 (X_j at So[i]); bottom j = NB - 2 - i (Y_j at So[NB - 2 - i])
+    const int n = top ? m - 1 : NB - 2 - m;
+    ChunkStream<T, KE> X{top ? Xs : Xs + (size_t)(NB - 2) * 81, top ? 81L : -81L, n, ring, {}, {}};
+    X.issue(0);
+    X.land(0);
+    for (int c = 0; c * KE < n; ++c) {
+        X.issue(c + 1);
+        wave_sync();
+        for (int q = 0; q < KE; ++q) {
+            const int i = c * KE + q;
+            if (i >= n) break;
+            const int j = top ? i + 1 : NB - 2 - i, jp = top ? j - 1 : j + 1;
             if (lane < 9) {
-                const LdsT<T> *yp = vb + (size_t)(j - 1) * 9;
-                T v = vb[(size_t)j * 9 + lane];
-                for (int q = 0; q < 9; ++q) v = fma(-cur[q], yp[q], v);
-                vb[(size_t)j * 9 + lane] = v;
+                const LdsT<T> *xr = X.blk(i) + lr * 9;
+                const LdsT<T> *yp = vb + jp * 9;
+                T xv[9], yv[9];
+#pragma unroll
+                for (int e = 0; e < 9; ++e) { xv[e] = xr[e]; yv[e] = yp[e]; }
+                const T bj = vb[j * 9 + lane];
+                T s0 = xv[0] * yv[0], s1 = xv[1] * yv[1], s2 = xv[2] * yv[2];
+#pragma unroll
+                for (int e = 3; e < 9; e += 3) {
+                    s0 = fma(xv[e], yv[e], s0); s1 = fma(xv[e + 1], yv[e + 1], s1); s2 = fma(xv[e + 2], yv[e + 2], s2);
+                }
+                vb[j * 9 + lane] = bj - (s0 + s1 + s2);
             }
             wave_sync();
         }
-    } else {
-        if (NB - 2 > m) ld_row(Xs + (size_t)(NB - 2) * 81 + lr * 9, nx);     // Y_{NB-2} at So[NB-2]
-        for (int j = NB - 2; j > m; --j) {
-            for (int q = 0; q < 9; ++q) cur[q] = nx[q];
-            if (j - 1 > m) ld_row(Xs + (size_t)(j - 1) * 81 + lr * 9, nx);
-            if (lane < 9) {
-                const LdsT<T> *yn = vb + (size_t)(j + 1) * 9;
-                T v = vb[(size_t)j * 9 + lane];
-                for (int q = 0; q < 9; ++q) v = fma(-cur[q], yn[q], v);
-                vb[(size_t)j * 9 + lane] = v;
-            }
-            wave_sync();
-        }
+        X.land(c + 1);
     }
+    wave_sync();
 }
-template <typename T, typename PS>
-__device__ void tw_solve_meet(const PS *Ii, const T *Xs, int NB, int m, LdsT<T> *vb, LdsT<T> *sh) {
+template <typename T>
+__device__ void tw_solve_meet(const T *Ii, const T *Xs, int NB, int m, LdsT<T> *vb, LdsT<T> *sh) {
     const int lane = threadIdx.x & 63;
     if (lane < 9) {
-        T v = vb[(size_t)m * 9 + lane];
+        T v = vb[m * 9 + lane];
         const T *X = Xs + (size_t)(m - 1) * 81 + lane * 9, *Y = Xs + (size_t)m * 81 + lane * 9;
-        const LdsT<T> *yp = vb + (size_t)(m - 1) * 9, *yn = vb + (size_t)(m + 1) * 9;
+        const LdsT<T> *yp = vb + (m - 1) * 9, *yn = vb + (m + 1) * 9;
         for (int q = 0; q < 9; ++q) v = fma(-X[q], yp[q], fma(-Y[q], yn[q], v));
         sh[lane] = v;
     }
     wave_sync();
     if (lane < 9) {
-        const PS *I = Ii + (size_t)m * 81 + lane * 9;
+        const T *I = Ii + (size_t)m * 81 + lane * 9;
         T v = T(0);
         for (int q = 0; q < 9; ++q) v = fma(I[q], sh[q], v);
-        vb[(size_t)m * 9 + lane] = v;
+        vb[m * 9 + lane] = v;
     }
     wave_sync();
 }
-template <typename T, typename PS>
-__device__ void tw_solve_back(const PS *Ii, const T *Xs, T *dnu, int NB, int m, LdsT<T> *vb) {
+template <typename T>
+__device__ void tw_solve_back(const T *Ii, const T *Xs, int NB, int m, LdsT<T> *vb, LdsT<T> *ring) {
     const int lane = threadIdx.x & 63;
     const bool top = (threadIdx.x >> 6) == 0;
     const int lr = lane < 9 ? lane : 0;
-    T nx[9], cur[9];
-    if (top) {
-        if (m >= 1) ld_col(Xs + (size_t)(m - 1) * 81 + lr, nx);         // X_m at So[m-1]
-        for (int j = m - 1; j >= 0; --j) {
-            for (int q = 0; q < 9; ++q) cur[q] = nx[q];
-            if (j >= 1) ld_col(Xs + (size_t)(j - 1) * 81 + lr, nx);     // X_j at So[j-1]
+    // step i: top j = m - 1 - i (I_j, X_{j+1} at So[j]); bottom j = m + 1 + i (I_j, Y_{j-1} at So[j-1])
+    const int n = top ? m : NB - 1 - m;
+    ChunkStream<T, KB> I{Ii + (size_t)(top ? m - 1 : m + 1) * 81, top ? -81L : 81L, n, ring, {}, {}};
+    ChunkStream<T, KB> X{Xs + (size_t)(top ? m - 1 : m) * 81, top ? -81L : 81L, n, ring + 2 * KB * RSLOT, {}, {}};
+    I.issue(0);
+    X.issue(0);
+    I.land(0);
+    X.land(0);
+    for (int c = 0; c * KB < n; ++c) {
+        I.issue(c + 1);
+        X.issue(c + 1);
+        wave_sync();
+        for (int q = 0; q < KB; ++q) {
+            const int i = c * KB + q;
+            if (i >= n) break;
+            const int j = top ? m - 1 - i : m + 1 + i, jn = top ? j + 1 : j - 1;
             T v = T(0);
             if (lane < 9) {
-                const PS *I = Ii + (size_t)j * 81 + lane * 9;   // symmetric: row == column
-                const LdsT<T> *y = vb + (size_t)j * 9;
-                for (int q = 0; q < 9; ++q) v = fma(I[q], y[q], v);
-                const LdsT<T> *xn = vb + (size_t)(j + 1) * 9;
-                for (int q = 0; q < 9; ++q) v = fma(-cur[q], xn[q], v);
+                const LdsT<T> *ir = I.blk(i) + lr * 9;    // symmetric: row == column
+                const LdsT<T> *xb = X.blk(i);
+                const LdsT<T> *y = vb + j * 9, *xn = vb + jn * 9;
+                T iv[9], yv[9], xc[9], nv[9];
+#pragma unroll
+                for (int e = 0; e < 9; ++e) { iv[e] = ir[e]; yv[e] = y[e]; xc[e] = xb[e * 9 + lr]; nv[e] = xn[e]; }
+                T s0 = iv[0] * yv[0], s1 = -(xc[0] * nv[0]);
+#pragma unroll
+                for (int e = 1; e < 9; ++e) { s0 = fma(iv[e], yv[e], s0); s1 = fma(-xc[e], nv[e], s1); }
+                v = s0 + s1;
             }
             wave_sync();
-            if (lane < 9) vb[(size_t)j * 9 + lane] = v;
+            if (lane < 9) vb[j * 9 + lane] = v;
             wave_sync();
         }
-    } else {
-        if (m + 1 < NB) ld_col(Xs + (size_t)m * 81 + lr, nx);            // Y_m at So[m]
-        for (int j = m + 1; j < NB; ++j) {
-            for (int q = 0; q < 9; ++q) cur[q] = nx[q];
-            if (j + 1 < NB) ld_col(Xs + (size_t)j * 81 + lr, nx);       // Y_j at So[j]
-            T v = T(0);
-            if (lane < 9) {
-                const PS *I = Ii + (size_t)j * 81 + lane * 9;
-                const LdsT<T> *y = vb + (size_t)j * 9;
-                for (int q = 0; q < 9; ++q) v = fma(I[q], y[q], v);
-                const LdsT<T> *xp = vb + (size_t)(j - 1) * 9;
-                for (int q = 0; q < 9; ++q) v = fma(-cur[q], xp[q], v);
-            }
-            wave_sync();
-            if (lane < 9) vb[(size_t)j * 9 + lane] = v;
-            wave_sync();
-        }
+        I.land(c + 1);
+        X.land(c + 1);
     }
-    const int lo = top ? 0 : m, hi = top ? m : NB;
-    for (int e = lo * 9 + lane; e < hi * 9; e += WAVE) dnu[e] = vb[e];
+    wave_sync();
 }
 
 // r_hat = r_i - r_c / lambda for the rows of knot k  (rc supplied per mode)
 template <typename T, int ROBOT>
 __device__ void rhat_rows(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu, T *rh) {
     constexpr int NI = Rows<ROBOT>::NI;
-    const T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
-    const T *rdi = C.ws + C.L.rdi + (size_t)k * NI;
-    const T *dsa = C.ws + C.L.dsa + (size_t)k * NI, *dla = C.ws + C.L.dla + (size_t)k * NI;
+    const SV<T> s = C.kv(WF(s), k), lm = C.kv(WF(l), k), rdi = C.kv(WF(rdi), k);
+    const SV<T> dsa = C.kv(WF(dsa), k), dla = C.kv(WF(dla), k);
     const unsigned msk = C.cmask(k);
     for (int r = 0; r < NI; ++r) {
         const bool pr = Ctx<T, ROBOT>::present_m(msk, r);
-        T rc = s[r] * lm[r];
+        const T sr = s[r], lr = lm[r];
+        T rc = sr * lr;
         if (corr) rc += dsa[r] * dla[r] - sigma_mu;
-        const T v = rdi[r] - fdiv(rc, pr ? lm[r] : T(1));
+        const T v = rdi[r] - fdiv(rc, pr ? lr : T(1));
         rh[r] = pr ? v : T(0);
     }
 }
 
 // (5a) particular solution w = Phi^-1 (r_d + G' D rhat) (friction rows in push-through form)
-template <typename T, int ROBOT> __device__ void phase_w(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu) {
+template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_w(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu) {
     using R_ = Rows<ROBOT>;
     constexpr int NI = R_::NI, NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
     const int N = C.N;
@@ -919,10 +1005,10 @@ template <typename T, int ROBOT> __device__ void phase_w(const Ctx<T, ROBOT> &C,
     T rh[NI];
     rhat_rows(C, k, corr, sigma_mu, rh);   // kept for phase_dz (stored below)
     T rdx[9], fxd[6], rdu[NU];
-    ldv(C.ws + C.L.rdx + (size_t)k * 9, rdx);
-    ldv(C.ws + C.L.facx + (size_t)k * FX, fxd);
-    if (hu) ldv(C.ws + C.L.rdu + (size_t)k * NU, rdu);
-    const T rdt = C.ws[C.L.rdt + k];
+    ldv(C.kv(WF(rdx), k), rdx);
+    ldv(C.kv(WF(facx), k), fxd);
+    ldv(C.kv(WF(rdu), k), rdu);   // k = N: unused
+    const T rdt = C.kv(WF(rdt), k)[0];
     T wx[9], wt;
     for (int i = 0; i < 6; ++i) wx[i] = fxd[i] * rdx[i];
     {   // (L, t): w = -(local solve with v = -r_d)
@@ -937,7 +1023,7 @@ template <typename T, int ROBOT> __device__ void phase_w(const Ctx<T, ROBOT> &C,
         T vu[NU];
         for (int i = 0; i < NU; ++i) vu[i] = rdu[i];
         if (ROBOT == 1) {   // CoP rows (D-form, folded into W_cop); absent rows: lambda = 0 -> D = 0, rhat = 0
-            const T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
+            const SV<T> s = C.kv(WF(s), k), lm = C.kv(WF(l), k);
             for (int c = 0; c < NC; ++c)
                 for (int dd = 0; dd < 2; ++dd) {
                     const int r0 = R_::CP + 4 * c + 2 * dd;
@@ -947,9 +1033,8 @@ template <typename T, int ROBOT> __device__ void phase_w(const Ctx<T, ROBOT> &C,
         phi_solve_u(C, k, vu, ou);
         for (int c = 0; c < NC; ++c) {
             // inactive contacts: Gw = 0, Kinv = I and rhat = 0, so they contribute nothing
-            const T *fu = C.ws + C.L.facu + ((size_t)k * NC + c) * FU;
             T g[22];
-            ldv(fu, g);
+            ldv(C.kv(WF(facu), k) + c * FU, g);
             T kr[4];
             for (int r = 0; r < 4; ++r) {
                 T acc = T(0);
@@ -964,29 +1049,32 @@ template <typename T, int ROBOT> __device__ void phase_w(const Ctx<T, ROBOT> &C,
         }
     }
     // stores
-    stv(C.ws + C.L.wx + (size_t)k * 9, wx);
-    C.ws[C.L.wt + k] = wt;
-    if (hu) stv(C.ws + C.L.wu + (size_t)k * NU, ou);
-    stv(C.ws + C.L.rh + (size_t)k * NI, rh);
+    stv(C.kv(WF(wx), k), wx);
+    C.kv(WF(wt), k)[0] = wt;
+    if (hu) stv(C.kv(WF(wu), k), ou);
+    stv(C.kv(WF(rh), k), rh);
 }
 
 
-// (5b) Schur right-hand side blocks owned by knot k: rhs = r_e - E w
-template <typename T, int ROBOT> __device__ void phase_rhs(const Ctx<T, ROBOT> &C, int k) {
+// (5b) Schur right-hand side blocks owned by knot k: rhs = r_e - E w, written into the LDS vector
+template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_rhs(const Ctx<T, ROBOT> &C, int k) {
     using S = Stage<ROBOT>;
     const int N = C.N;
-    const T *wx = C.ws + C.L.wx + (size_t)k * 9;
-    const T *rde = C.ws + C.L.rde;
-    T *rhs = C.ws + C.L.rhs;
-    if (k == 0) for (int i = 0; i < 9; ++i) rhs[i] = rde[i] - wx[i];
-    if (k == N) for (int i = 0; i < 9; ++i) rhs[(size_t)(N + 1) * 9 + i] = rde[(size_t)(N + 1) * 9 + i] - wx[i];
+    T wx[9], wx1[9], wu[NU], r0[9], r1[9];
+    ldv(C.kv(WF(wx), k), wx);
+    ldv(C.kv(WF(wx), k < N ? k + 1 : k), wx1);
+    ldv(C.kv(WF(wu), k), wu);
+    ldv(C.bv(WF(rde), k == N ? N + 1 : 0), r0);   // boundary rows (k = 0: init, k = N: final)
+    ldv(C.bv(WF(rde), k < N ? 1 + k : 0), r1);     // dynamics rows of knot k
+    LdsT<T> *vb = C.vb;
+    if (k == 0) for (int i = 0; i < 9; ++i) vb[i] = r0[i] - wx[i];
+    if (k == N) for (int i = 0; i < 9; ++i) vb[(N + 1) * 9 + i] = r0[i] - wx[i];
     if (k < N) {
         T ax[9], bu[9];
-        opA(C.st(k) + S::W, C.beta, wx, ax);
-        opB<T, ROBOT>(C.st(k), C.ws + C.L.wu + (size_t)k * NU, bu);
-        const T *wx1 = wx + 9;
-        for (int i = 0; i < 9; ++i)
-            rhs[(size_t)(1 + k) * 9 + i] = rde[(size_t)(1 + k) * 9 + i] - (ax[i] + bu[i] - wx1[i]);
+        const auto st = C.st(k);
+        opA(st + S::W, C.beta, wx, ax);
+        opB<T, ROBOT>(st, wu, bu);
+        for (int i = 0; i < 9; ++i) vb[(1 + k) * 9 + i] = r1[i] - (ax[i] + bu[i] - wx1[i]);
     }
 }
 
@@ -994,14 +1082,16 @@ template <typename T, int ROBOT> __device__ void phase_rhs(const Ctx<T, ROBOT> &
 // rows of knot k: ds = -r_i - G dz; dlambda from the push-through solves (TR, slack: dlt, dls;
 // friction: Kinv (Gw v + rhat) with v = -(rdu + E'dnu_u) on the forces) or the D-form (CoP);
 // returns the largest step keeping s, lambda >= 0.  The memory operands are restrict-qualified
-// so the loads of s, lambda, r_i, the stage and the friction factors are not held behind the
-// stores of ds, dlambda.  Inactive contacts: G = Gw = 0, Kinv = I, rhat = 0 -> zero steps.
+// (field-major records, field f at p[f * ld]) so the loads of s, lambda, r_i, the stage and the
+// friction factors are not held behind the stores of ds, dlambda.  Inactive contacts:
+// G = Gw = 0, Kinv = I, rhat = 0 -> zero steps.
 template <typename T, int ROBOT>
 __device__ __forceinline__ T dz_rows(const Ctx<T, ROBOT> &C, int k, const T (&dx)[9], T dtt, const T (&du)[NU],
                                      const T (&eu)[NU], const T (&dlt)[8], T dls, const T (&rh)[Rows<ROBOT>::NI],
-                                     const T *__restrict__ st, const T *__restrict__ fu, const T *__restrict__ rdu,
-                                     const T *__restrict__ rdi, const T *__restrict__ sv, const T *__restrict__ lm,
-                                     T *__restrict__ ds, T *__restrict__ dl) {
+                                     const int ld, const T *__restrict__ st, const T *__restrict__ fu,
+                                     const T *__restrict__ rdu, const T *__restrict__ rdi,
+                                     const T *__restrict__ sv, const T *__restrict__ lm, T *__restrict__ ds,
+                                     T *__restrict__ dl) {
     using S = Stage<ROBOT>;
     using R_ = Rows<ROBOT>;
     constexpr int NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
@@ -1009,11 +1099,11 @@ __device__ __forceinline__ T dz_rows(const Ctx<T, ROBOT> &C, int k, const T (&dx
     const unsigned msk = C.cmask(k);
     T amax = T(1);
     auto emit = [&](int r, bool pr, T g, T dlr) {
-        const T dsr = pr ? -rdi[r] - g : T(0);
-        ds[r] = dsr;
-        dl[r] = dlr;
+        const T dsr = pr ? -rdi[r * ld] - g : T(0);
+        ds[r * ld] = dsr;
+        dl[r * ld] = dlr;
         // branch-free ratio tests (selects keep the row loop one basic block)
-        const T qs = fdiv(-sv[r], dsr < T(0) ? dsr : T(-1)), ql = fdiv(-lm[r], dlr < T(0) ? dlr : T(-1));
+        const T qs = fdiv(-sv[r * ld], dsr < T(0) ? dsr : T(-1)), ql = fdiv(-lm[r * ld], dlr < T(0) ? dlr : T(-1));
         amax = fmin(amax, fmin(dsr < T(0) ? qs : T(1), dlr < T(0) ? ql : T(1)));
     };
 #pragma unroll
@@ -1024,18 +1114,19 @@ __device__ __forceinline__ T dz_rows(const Ctx<T, ROBOT> &C, int k, const T (&dx
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         const bool pr = hu && ((msk >> c) & 1u);
-        const T *cs = st + S::CON + S::CS * c;
-        const T *g = fu + c * FU;
+        const T *cs = st + (S::CON + S::CS * c) * ld;
+        const T *g = fu + c * FU * ld;
         T vf[3];
-        for (int i = 0; i < 3; ++i) vf[i] = hu ? -(rdu[NUPC * c + FO + i] + eu[NUPC * c + FO + i]) : T(0);
+        for (int i = 0; i < 3; ++i) vf[i] = hu ? -(rdu[(NUPC * c + FO + i) * ld] + eu[NUPC * c + FO + i]) : T(0);
         T z[4];
         for (int r = 0; r < 4; ++r)
-            z[r] = g[3 * r] * vf[0] + g[3 * r + 1] * vf[1] + g[3 * r + 2] * vf[2] + rh[R_::FR + 4 * c + r];
+            z[r] = g[(3 * r) * ld] * vf[0] + g[(3 * r + 1) * ld] * vf[1] + g[(3 * r + 2) * ld] * vf[2] +
+                   rh[R_::FR + 4 * c + r];
         for (int r = 0; r < 4; ++r) {
             T acc = T(0);
-            for (int q = 0; q < 4; ++q) acc += g[12 + p4(r, q)] * z[q];
-            const T gr = cs[S::G + 3 * r] * du[NUPC * c + FO] + cs[S::G + 3 * r + 1] * du[NUPC * c + FO + 1] +
-                         cs[S::G + 3 * r + 2] * du[NUPC * c + FO + 2];
+            for (int q = 0; q < 4; ++q) acc += g[(12 + p4(r, q)) * ld] * z[q];
+            const T gr = cs[(S::G + 3 * r) * ld] * du[NUPC * c + FO] + cs[(S::G + 3 * r + 1) * ld] * du[NUPC * c + FO + 1] +
+                         cs[(S::G + 3 * r + 2) * ld] * du[NUPC * c + FO + 2];
             emit(R_::FR + 4 * c + r, pr, gr, hu ? acc : T(0));
         }
     }
@@ -1046,7 +1137,7 @@ __device__ __forceinline__ T dz_rows(const Ctx<T, ROBOT> &C, int k, const T (&dx
             for (int q = 0; q < 4; ++q) {
                 const int r = R_::CP + 4 * c + q, dd = q / 2;
                 const T gr = (q % 2 == 0) ? du[NUPC * c + dd] : -du[NUPC * c + dd];
-                emit(r, pr, gr, pr ? C.Dform(lm[r], sv[r]) * (gr + rh[r]) : T(0));
+                emit(r, pr, gr, pr ? C.Dform(lm[r * ld], sv[r * ld]) * (gr + rh[r]) : T(0));
             }
         }
     }
@@ -1054,29 +1145,28 @@ __device__ __forceinline__ T dz_rows(const Ctx<T, ROBOT> &C, int k, const T (&dx
 }
 
 template <typename T, int ROBOT>
-__device__ T phase_dz(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu) {
+__device__ PHASE_ATTR T phase_dz(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu) {
     using S = Stage<ROBOT>;
     using R_ = Rows<ROBOT>;
-    constexpr int NI = R_::NI, NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
+    constexpr int NI = R_::NI;
     const int N = C.N;
     const bool hu = k < N;
-    // E' dnu at knot k; the knot-type cases are selects over in-range blocks (one basic block)
-    const T *dnu = C.ws + C.L.dnu;
+    // E' dnu at knot k from the LDS blocks k, k+1 (k = 0: block 0 is the init rows; k = N: block
+    // N+1 the final rows); the knot-type cases are selects (one basic block)
+    const LdsT<T> *vb = C.vb;
     const int kc = hu ? k : 0;   // k = N: no controls or contacts (stage / factor records unused)
-    T ex[9], eu[NU], a[9], d0[9], dk[9], dN[9];
-    opAT(C.st(k) + S::W, C.beta, dnu + (size_t)(1 + k) * 9, a);   // k = N: block N+1 (unused)
-    opBT<T, ROBOT>(C.st(kc), dnu + (size_t)(1 + kc) * 9, eu);
-    ldv(dnu, d0);
-    ldv(dnu + (size_t)k * 9, dk);
-    ldv(dnu + (size_t)(N + 1) * 9, dN);
+    T dk[9], d1[9], ex[9], eu[NU], a[9];
+    for (int i = 0; i < 9; ++i) { dk[i] = vb[k * 9 + i]; d1[i] = vb[(k + 1) * 9 + i]; }
+    opAT(C.st(k) + S::W, C.beta, d1, a);
+    opBT<T, ROBOT>(C.st(kc), d1, eu);
     for (int i = 0; i < 9; ++i)
-        ex[i] = (k == 0 ? d0[i] : T(0)) + (hu ? a[i] : T(0)) - (k >= 1 ? dk[i] : T(0)) + (k == N ? dN[i] : T(0));
+        ex[i] = (k == 0 ? dk[i] : -dk[i]) + (hu ? a[i] : T(0)) + (k == N ? d1[i] : T(0));
     T rh[NI], rdx[9], fxd[6], wu[NU];
-    ldv(C.ws + C.L.rh + (size_t)k * NI, rh);   // this step's rhat, from phase_w
-    ldv(C.ws + C.L.rdx + (size_t)k * 9, rdx);
-    ldv(C.ws + C.L.facx + (size_t)k * FX, fxd);
-    ldv(C.ws + C.L.wu + (size_t)kc * NU, wu);
-    const T rdt = C.ws[C.L.rdt + k];
+    ldv(C.kv(WF(rh), k), rh);   // this step's rhat, from phase_w
+    ldv(C.kv(WF(rdx), k), rdx);
+    ldv(C.kv(WF(facx), k), fxd);
+    ldv(C.kv(WF(wu), kc), wu);
+    const T rdt = C.kv(WF(rdt), k)[0];
     T dx[9], dtt, du[NU], dlt[8], dls;
     for (int i = 0; i < 6; ++i) dx[i] = -fxd[i] * (rdx[i] + ex[i]);
     {
@@ -1088,72 +1178,73 @@ __device__ T phase_dz(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu) {
         phi_solve_u(C, kc, eu, au);
         for (int i = 0; i < NU; ++i) du[i] = hu ? -wu[i] - au[i] : T(0);
     }
-    stv(C.ws + C.L.dx + (size_t)k * 9, dx);
-    C.ws[C.L.dt + k] = dtt;
-    if (hu) stv(C.ws + C.L.du + (size_t)k * NU, du);
-    return dz_rows<T, ROBOT>(C, k, dx, dtt, du, eu, dlt, dls, rh, C.st(k), C.ws + C.L.facu + (size_t)kc * NC * FU,
-                             C.ws + C.L.rdu + (size_t)kc * NU, C.ws + C.L.rdi + (size_t)k * NI,
-                             C.ws + C.L.s + (size_t)k * NI, C.ws + C.L.l + (size_t)k * NI,
-                             C.ws + (corr ? C.L.ds : C.L.dsa) + (size_t)k * NI,
-                             C.ws + (corr ? C.L.dl : C.L.dla) + (size_t)k * NI);
+    constexpr int ld = KPC;
+    const T amax = dz_rows<T, ROBOT>(C, k, dx, dtt, du, eu, dlt, dls, rh, ld, C.stage + kc,
+                                     C.ws + WF(facu) * KPC + kc, C.ws + WF(rdu) * KPC + kc, C.ws + WF(rdi) * KPC + k,
+                                     C.ws + WF(s) * KPC + k, C.ws + WF(l) * KPC + k, C.ws + (corr ? WF(ds) : WF(dsa)) * KPC + k,
+                                     C.ws + (corr ? WF(dl) : WF(dla)) * KPC + k);
+    stv(C.kv(WF(dx), k), dx);
+    C.kv(WF(dt), k)[0] = dtt;
+    if (hu) stv(C.kv(WF(du), k), du);
+    return amax;
 }
 
 template <typename T, int ROBOT> __device__ T mu_after(const Ctx<T, ROBOT> &C, int k, T a) {
     constexpr int NI = Rows<ROBOT>::NI;
-    const T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
-    const T *ds = C.ws + C.L.dsa + (size_t)k * NI, *dl = C.ws + C.L.dla + (size_t)k * NI;
+    const SV<T> s = C.kv(WF(s), k), lm = C.kv(WF(l), k), ds = C.kv(WF(dsa), k), dl = C.kv(WF(dla), k);
     T acc = T(0);
     for (int r = 0; r < NI; ++r)
         acc += (s[r] + a * ds[r]) * (lm[r] + a * dl[r]);   // absent rows: lambda = dl = 0
     return acc;
 }
 
-template <typename T, int ROBOT> __device__ void phase_update(const Ctx<T, ROBOT> &C, int k, T a, bool affine = false) {
+// z, nu, s, lambda += a * direction (dnu from the LDS vector)
+template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_update(const Ctx<T, ROBOT> &C, int k, T a, bool affine = false) {
     constexpr int NI = Rows<ROBOT>::NI;
     const int N = C.N;
+    const LdsT<T> *vb = C.vb;
     {
-        T x[9], dx[9];
+        T x[9], dx[9], n1[9], n0[9], u[NU], du[NU];
         ldv(C.var_x(k), x);
-        ldv(C.ws + C.L.dx + (size_t)k * 9, dx);
-        const T t = C.ws[C.L.t + k], dt = C.ws[C.L.dt + k];
-        T n1[9], dn1[9], n0[9], dn0[9];
-        ldv(C.ws + C.L.nu + (size_t)(1 + k) * 9, n1);        // k < N: dynamics block k; k = N: final
-        ldv(C.ws + C.L.dnu + (size_t)(1 + k) * 9, dn1);
-        if (k == 0) { ldv(C.ws + C.L.nu, n0); ldv(C.ws + C.L.dnu, dn0); }
-        T u[NU], du[NU];
-        if (k < N) { ldv(C.var_u(k), u); ldv(C.ws + C.L.du + (size_t)k * NU, du); }
-        for (int i = 0; i < 9; ++i) { x[i] += a * dx[i]; n1[i] += a * dn1[i]; n0[i] += a * dn0[i]; }
+        ldv(C.kv(WF(dx), k), dx);
+        const T t = C.kv(WF(t), k)[0], dt = C.kv(WF(dt), k)[0];
+        ldv(C.bv(WF(nu), 1 + k), n1);        // k < N: dynamics block k; k = N: final
+        ldv(C.bv(WF(nu), 0), n0);
+        ldv(C.var_u(k), u);
+        ldv(C.kv(WF(du), k), du);
+        for (int i = 0; i < 9; ++i) {
+            x[i] += a * dx[i];
+            n1[i] += a * vb[(1 + k) * 9 + i];
+            n0[i] += a * vb[i];
+        }
         for (int i = 0; i < NU; ++i) u[i] += a * du[i];
         stv(C.var_x(k), x);
-        C.ws[C.L.t + k] = t + a * dt;
-        stv(C.ws + C.L.nu + (size_t)(1 + k) * 9, n1);
-        if (k == 0) stv(C.ws + C.L.nu, n0);
+        C.kv(WF(t), k)[0] = t + a * dt;
+        stv(C.bv(WF(nu), 1 + k), n1);
+        if (k == 0) stv(C.bv(WF(nu), 0), n0);
         if (k < N) stv(C.var_u(k), u);
     }
-    T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
-    const T *ds = C.ws + (affine ? C.L.dsa : C.L.ds) + (size_t)k * NI;
-    const T *dl = C.ws + (affine ? C.L.dla : C.L.dl) + (size_t)k * NI;
-    T sv[NI], dsv[NI];   // absent rows: ds = dl = 0 (s stays 1, lambda 0)
+    const SV<T> s = C.kv(WF(s), k), lm = C.kv(WF(l), k);
+    const SV<T> ds = C.kv(affine ? WF(dsa) : WF(ds), k), dl = C.kv(affine ? WF(dla) : WF(dl), k);
+    T sv[NI], dsv[NI], lv[NI], dlv[NI];   // absent rows: ds = dl = 0 (s stays 1, lambda 0)
     ldv(s, sv); ldv(ds, dsv);
-    for (int r = 0; r < NI; ++r) sv[r] += a * dsv[r];
-    T lv[NI], dlv[NI];
     ldv(lm, lv); ldv(dl, dlv);
+    for (int r = 0; r < NI; ++r) { sv[r] += a * dsv[r]; lv[r] += a * dlv[r]; }
     stv(s, sv);
-    for (int r = 0; r < NI; ++r) lv[r] += a * dlv[r];
     stv(lm, lv);
 }
 
 
 // initialization step: full Newton step for z and nu; s = h - gz at the new z; lambda += dlambda.
 // vmax receives (max -s, max -lambda) over this knot's rows.
-template <typename T, int ROBOT> __device__ void phase_init_step(const Ctx<T, ROBOT> &C, int k, T (&vmax)[2]) {
+template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_init_step(const Ctx<T, ROBOT> &C, int k, T (&vmax)[2]) {
     constexpr int NI = Rows<ROBOT>::NI;
     phase_update<T, ROBOT>(C, k, T(1), true);   // z, nu, lambda: full affine step; s recomputed below
-    const int N = C.N;
-    const T *x = C.var_x(k);
-    const T t = C.ws[C.L.t + k];
-    const T *u = C.var_u(k < N ? k : 0);   // k = N: rows of u are absent (values unused)
-    T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
+    T x[9], u[NU];
+    ldv(C.var_x(k), x);
+    ldv(C.var_u(k), u);   // k = N: rows of u are absent (values unused)
+    const T t = C.kv(WF(t), k)[0];
+    const SV<T> s = C.kv(WF(s), k), lm = C.kv(WF(l), k);
     for (int r = 0; r < NI; ++r) {
         if (!C.present(k, r)) continue;
         s[r] = -C.gz(k, r, x, t, u, true);
@@ -1161,9 +1252,9 @@ template <typename T, int ROBOT> __device__ void phase_init_step(const Ctx<T, RO
         vmax[1] = fmax(vmax[1], -lm[r]);
     }
 }
-template <typename T, int ROBOT> __device__ void phase_init_shift(const Ctx<T, ROBOT> &C, int k, T sh_s, T sh_l) {
+template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_init_shift(const Ctx<T, ROBOT> &C, int k, T sh_s, T sh_l) {
     constexpr int NI = Rows<ROBOT>::NI;
-    T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
+    const SV<T> s = C.kv(WF(s), k), lm = C.kv(WF(l), k);
     for (int r = 0; r < NI; ++r) {
         if (!C.present(k, r)) continue;
         s[r] += sh_s;
@@ -1172,7 +1263,7 @@ template <typename T, int ROBOT> __device__ void phase_init_shift(const Ctx<T, R
 }
 
 // ------------------------------------------------------------------ kernel
-template <typename T, int ROBOT, bool SL>
+template <typename T, int ROBOT>
 __global__ void __launch_bounds__(NT) k_qp_ipm(DevBuf<T> d, int only_active, int max_iter, T eps_abs, T eps_rel,
                                                T eta) {
     extern __shared__ __attribute__((aligned(16))) unsigned char dsmem[];
@@ -1183,10 +1274,9 @@ __global__ void __launch_bounds__(NT) k_qp_ipm(DevBuf<T> d, int only_active, int
     __shared__ T red[8 * (NT / 64)];
     __shared__ T sh[2 * TW_SCRATCH];
     const int tid = threadIdx.x, N = d.N, K1 = N + 1, NB = N + 2, NBm = NB / 2;
-    Ctx<T, ROBOT> C{N, nullptr, nullptr, nullptr, nullptr, T(0), T(0), nullptr, WsLayout(N, NI, Robot<ROBOT>::NC),
-                    nullptr, nullptr, T(0)};
+    Ctx<T, ROBOT> C{N, nullptr, nullptr, nullptr, nullptr, T(0), T(0), nullptr, nullptr, nullptr, nullptr, T(0)};
     C.prm = d.params + d.class_id[b];
-    C.stage = d.stage + (size_t)b * K1 * Stage<ROBOT>::SIZE;
+    C.stage = d.stage + (size_t)b * Stage<ROBOT>::SIZE * KPC;
     C.logic = d.logic + (size_t)b * N * Robot<ROBOT>::NC;
     C.xbar = d.Xbar + (size_t)b * K1 * 9;
     C.cw = d.cw[b];
@@ -1197,11 +1287,12 @@ __global__ void __launch_bounds__(NT) k_qp_ipm(DevBuf<T> d, int only_active, int
         C.dcap = T(1e12) * wmax;
     }
     C.ws = d.ws + (size_t)b * d.ws_stride;
-    T *vbuf = reinterpret_cast<T *>(dsmem);
-    LdsT<T> *vbl = (LdsT<T> *)vbuf, *shl = (LdsT<T> *)sh;
-    // the Schur inverses sit in LDS when they fit (SL); the off-diagonal factors always in HBM
-    C.Sd = SL ? vbuf + (((size_t)NB * 9 + 7) & ~size_t(7)) : C.ws + C.L.Sd;
-    C.So = C.ws + C.L.So;
+    // dynamic LDS: the (N+2) x 9 Schur vector, then two block rings per wave for the sweeps
+    LdsT<T> *shl = (LdsT<T> *)sh;
+    C.vb = (LdsT<T> *)reinterpret_cast<T *>(dsmem);
+    LdsT<T> *ring = C.vb + ((NB * 9 + 7) & ~7) + (tid >> 6) * SWEEP_LDS;
+    C.Sd = C.ws + Ws<ROBOT>::Sd;
+    C.So = C.ws + Ws<ROBOT>::So;
 #ifdef CMPC_STAMPS
     unsigned long long t_prev = __builtin_amdgcn_s_memtime(), t_acc[12] = {};
 #define STAMP(i)                                                               \
@@ -1215,20 +1306,24 @@ __global__ void __launch_bounds__(NT) k_qp_ipm(DevBuf<T> d, int only_active, int
 #endif
     // ---- starting point of the initialization step: z = (xbar, ubar, 0), nu = 0, s = lambda = 1
     for (int k = tid; k < K1; k += NT) {
-        T *x = C.var_x(k);
+        const SV<T> x = C.var_x(k);
         for (int i = 0; i < 9; ++i) x[i] = C.xbar[(size_t)k * 9 + i];
-        C.ws[C.L.t + k] = T(0);
+        C.kv(WF(t), k)[0] = T(0);
         const T *ubar = d.Ubar + ((size_t)b * N + (k < N ? k : 0)) * NU;
-        if (k < N) { T *u = C.var_u(k); for (int i = 0; i < NU; ++i) u[i] = ubar[i]; }
-        T *s = C.ws + C.L.s + (size_t)k * NI, *lm = C.ws + C.L.l + (size_t)k * NI;
+        if (k < N) { const SV<T> u = C.var_u(k); for (int i = 0; i < NU; ++i) u[i] = ubar[i]; }
+        const SV<T> s = C.kv(WF(s), k), lm = C.kv(WF(l), k), dsa = C.kv(WF(dsa), k), dla = C.kv(WF(dla), k);
+        const unsigned msk = C.cmask(k);
         for (int r = 0; r < NI; ++r) {
             s[r] = T(1);
-            lm[r] = C.present(k, r) ? T(1) : T(0);
+            lm[r] = Ctx<T, ROBOT>::present_m(msk, r) ? T(1) : T(0);
+            dsa[r] = T(0);
+            dla[r] = T(0);
         }
-        T *dsa = C.ws + C.L.dsa + (size_t)k * NI, *dla = C.ws + C.L.dla + (size_t)k * NI;
-        for (int r = 0; r < NI; ++r) { dsa[r] = T(0); dla[r] = T(0); }
     }
-    for (int e = tid; e < NB * 9; e += NT) C.ws[C.L.nu + e] = T(0);
+    for (int j = tid; j < NB; j += NT) {
+        const SV<T> nu = C.bv(WF(nu), j);
+        for (int i = 0; i < 9; ++i) nu[i] = T(0);
+    }
     __syncthreads();
     int status = CMPC_QP_MAX_ITER, it = 0, stall = 0;
     T mu_prev = T(-1);
@@ -1264,15 +1359,9 @@ __global__ void __launch_bounds__(NT) k_qp_ipm(DevBuf<T> d, int only_active, int
         for (int k = tid; k < K1; k += NT) phase_sblock<T, ROBOT>(C, k);
         __syncthreads();
         STAMP(2);
-        if (SL) {
-            if (tid < 128) tw_factor_ends<T, LdsT<T>>((LdsT<T> *)C.Sd, C.So, NB, NBm, shl);
-            __syncthreads();
-            if (tid < 64) tw_factor_meet<T, LdsT<T>>((LdsT<T> *)C.Sd, C.So, NBm, shl);
-        } else {
-            if (tid < 128) tw_factor_ends<T, T>(C.Sd, C.So, NB, NBm, shl);
-            __syncthreads();
-            if (tid < 64) tw_factor_meet<T, T>(C.Sd, C.So, NBm, shl);
-        }
+        if (tid < 128) tw_factor_ends<T>(C.Sd, C.So, NB, NBm, shl);
+        __syncthreads();
+        if (tid < 64) tw_factor_meet<T>(C.Sd, C.So, NBm, shl);
         STAMP(3);
         __syncthreads();
         // ---- predictor (affine) and corrector
@@ -1285,18 +1374,11 @@ __global__ void __launch_bounds__(NT) k_qp_ipm(DevBuf<T> d, int only_active, int
             for (int k = tid; k < K1; k += NT) phase_rhs<T, ROBOT>(C, k);
             __syncthreads();
             STAMP(5);
-            if (tid < 128) tw_solve_elim<T>(C.So, C.ws + C.L.rhs, NB, NBm, vbl);
+            if (tid < 128) tw_solve_elim<T>(C.So, NB, NBm, C.vb, ring);
             __syncthreads();
-            if (SL) {
-                if (tid < 64) tw_solve_meet<T, LdsT<T>>((LdsT<T> *)C.Sd, C.So, NB, NBm, vbl, shl);
-                __syncthreads();
-                if (tid < 128) tw_solve_back<T, LdsT<T>>((LdsT<T> *)C.Sd, C.So, C.ws + C.L.dnu, NB, NBm, vbl);
-            } else {
-                if (tid < 64) tw_solve_meet<T, T>(C.Sd, C.So, NB, NBm, vbl, shl);
-                __syncthreads();
-                if (tid < 128) tw_solve_back<T, T>(C.Sd, C.So, C.ws + C.L.dnu, NB, NBm, vbl);
-            }
+            if (tid < 64) tw_solve_meet<T>(C.Sd, C.So, NB, NBm, C.vb, shl);
             __syncthreads();
+            if (tid < 128) tw_solve_back<T>(C.Sd, C.So, NB, NBm, C.vb, ring);
             STAMP(6);
             T am[1] = {T(1)};
             for (int k = tid; k < K1; k += NT) am[0] = fmin(am[0], phase_dz<T, ROBOT>(C, k, corr, sigma_mu));
@@ -1330,14 +1412,18 @@ __global__ void __launch_bounds__(NT) k_qp_ipm(DevBuf<T> d, int only_active, int
     }
     // ---- outputs: solution and multipliers
     for (int k = tid; k < K1; k += NT) {
-        const T *x = C.var_x(k);
+        T x[9], u[NU], lm[NI];
+        ldv(C.var_x(k), x);
+        ldv(C.var_u(k), u);
+        ldv(C.kv(WF(l), k), lm);
+        const unsigned msk = C.cmask(k);
         for (int i = 0; i < 9; ++i) d.xs[((size_t)b * K1 + k) * 9 + i] = x[i];
-        d.ts[(size_t)b * K1 + k] = C.ws[C.L.t + k];
-        if (k < N) { const T *u = C.var_u(k); for (int i = 0; i < NU; ++i) d.us[((size_t)b * N + k) * NU + i] = u[i]; }
-        const T *lm = C.ws + C.L.l + (size_t)k * NI;
-        for (int r = 0; r < NI; ++r) d.lams[((size_t)b * K1 + k) * NI + r] = C.present(k, r) ? lm[r] : T(0);
+        d.ts[(size_t)b * K1 + k] = C.kv(WF(t), k)[0];
+        if (k < N) for (int i = 0; i < NU; ++i) d.us[((size_t)b * N + k) * NU + i] = u[i];
+        for (int r = 0; r < NI; ++r)
+            d.lams[((size_t)b * K1 + k) * NI + r] = Ctx<T, ROBOT>::present_m(msk, r) ? lm[r] : T(0);
     }
-    for (int e = tid; e < NB * 9; e += NT) d.nus[(size_t)b * NB * 9 + e] = C.ws[C.L.nu + e];
+    for (int e = tid; e < NB * 9; e += NT) d.nus[(size_t)b * NB * 9 + e] = C.ws[(WF(nu) + e % 9) * KPC + e / 9];
     if (tid == 0) {
         d.qp_status[b] = status;
         d.qp_iters[b] = it;
@@ -1348,20 +1434,20 @@ __global__ void __launch_bounds__(NT) k_qp_ipm(DevBuf<T> d, int only_active, int
 #undef STAMP
 }
 
-#define INST(T, R)                                                                   \
-    template __global__ void k_qp_ipm<T, R, false>(DevBuf<T>, int, int, T, T, T);     \
-    template __global__ void k_qp_ipm<T, R, true>(DevBuf<T>, int, int, T, T, T);
+#define INST(T, R) template __global__ void k_qp_ipm<T, R>(DevBuf<T>, int, int, T, T, T);
 INST(double, 0)
 INST(double, 1)
 INST(float, 0)
 INST(float, 1)
 #undef INST
 
-size_t ipm_vec_lds_bytes(int N, int prec_bytes) { return (((size_t)(N + 2) * 9 + 7) & ~size_t(7)) * prec_bytes; }
-size_t ipm_schur_lds_bytes(int N, int prec_bytes) { return (size_t)(N + 2) * 81 * prec_bytes; }
+size_t ipm_lds_bytes(int N, int prec_bytes) {
+    return ((((size_t)(N + 2) * 9 + 7) & ~size_t(7)) + (size_t)(IPM_NT / 64) * SWEEP_LDS) * prec_bytes;
+}
 
 size_t ipm_workspace_elems(int N, int robot) {
-    return robot == 0 ? WsLayout(N, Rows<0>::NI, Robot<0>::NC).total : WsLayout(N, Rows<1>::NI, Robot<1>::NC).total;
+    (void)N;
+    return robot == 0 ? Ws<0>::total : Ws<1>::total;
 }
 
 }  // namespace cmpc
