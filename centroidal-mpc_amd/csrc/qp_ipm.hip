@@ -28,6 +28,9 @@
 #define PHASE_ATTR
 #endif
 #define WF(f) (Ws<ROBOT>::f)   // workspace field row
+#ifndef QP_MIN_WAVES
+#define QP_MIN_WAVES 1   // __launch_bounds__ waves per SIMD (2: 256 registers, four workgroups per CU)
+#endif
 
 namespace cmpc {
 
@@ -711,17 +714,32 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_sblock(const C
 // over the 64 lanes (SPD: no pivoting) with a pivot floor relative to the original diagonal
 // (near the solution of a degenerate QP the Schur blocks are differences of O(M) numbers).
 // Per-wave LDS scratch: A (current) | P (previous inverse) | Xb | Ob | Dd (original diagonal).
+template <typename T> __device__ __forceinline__ T dot9(const LdsT<T> *a, const LdsT<T> *b) {
+    T av[9], bv[9];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) { av[q] = a[q]; bv[q] = b[q]; }
+    T s0 = av[0] * bv[0], s1 = av[1] * bv[1], s2 = av[2] * bv[2];
+#pragma unroll
+    for (int q = 3; q < 9; q += 3) { s0 = fma(av[q], bv[q], s0); s1 = fma(av[q + 1], bv[q + 1], s1); s2 = fma(av[q + 2], bv[q + 2], s2); }
+    return s0 + s1 + s2;
+}
 constexpr int TW_SCRATCH = 4 * 88 + 16;
 
+// With vb != nullptr the step also runs the forward elimination of the right-hand side held in
+// vb (the predictor's, known before the factorization): y_j = b_j - X_j y_jx (top), or
+// b_j - Y_j y_jy (bottom), or at the meeting block x_m = I_m (b_m - X_m y_{m-1} - Y_m y_{m+1}),
+// with X_j / Y_j read from the LDS scratch while they are there.
 template <typename T>
 __device__ __forceinline__ void tw_step(T d0, T d1, const LdsT<T> *Op, const LdsT<T> *Ip, const LdsT<T> *Oq,
                                         const LdsT<T> *Iq, T *Xout, T *Yout, T *Iout, LdsT<T> *A, LdsT<T> *P,
-                                        LdsT<T> *Xb, LdsT<T> *Dd) {
+                                        LdsT<T> *Xb, LdsT<T> *Dd, LdsT<T> *vb = nullptr, int j = 0, int jx = 0,
+                                        int jy = 0) {
     const int lane = threadIdx.x & 63;
     const int e0 = lane, e1 = lane + 64;
     const bool has1 = e1 < 81;
     const int i0 = e0 / 9, c0 = e0 % 9, i1 = e1 / 9, c1 = e1 % 9;
     T a0 = d0, a1 = d1;
+    T rv = (vb && lane < 9) ? vb[j * 9 + lane] : T(0);   // b_j (fused elimination)
     if (e0 % 10 == 0) Dd[e0 / 10] = d0;
     if (e1 == 80) Dd[8] = d1;
     T x0 = T(0), x1 = T(0), y0 = T(0), y1 = T(0);
@@ -733,6 +751,7 @@ __device__ __forceinline__ void tw_step(T d0, T d1, const LdsT<T> *Op, const Lds
         Xb[e0] = x0;
         if (has1) Xb[e1] = x1;
         wave_sync();
+        if (vb && lane < 9) rv -= dot9(Xb + lane * 9, vb + jx * 9);
         for (int m = 0; m < 9; ++m) {
             a0 = fma(-Xb[i0 * 9 + m], Op[m * 9 + c0], a0);
             if (has1) a1 = fma(-Xb[i1 * 9 + m], Op[m * 9 + c1], a1);
@@ -747,6 +766,7 @@ __device__ __forceinline__ void tw_step(T d0, T d1, const LdsT<T> *Op, const Lds
         Xb[e0] = y0;
         if (has1) Xb[e1] = y1;
         wave_sync();
+        if (vb && lane < 9) rv -= dot9(Xb + lane * 9, vb + jy * 9);
         for (int m = 0; m < 9; ++m) {
             a0 = fma(-Xb[i0 * 9 + m], Oq[c0 * 9 + m], a0);
             if (has1) a1 = fma(-Xb[i1 * 9 + m], Oq[c1 * 9 + m], a1);
@@ -780,11 +800,20 @@ __device__ __forceinline__ void tw_step(T d0, T d1, const LdsT<T> *Op, const Lds
     if (has1) P[e1] = r1;
     Iout[e0] = r0;
     if (has1) Iout[e1] = r1;
+    if (vb) {
+        if (Op && Oq) {   // meeting block: x_m = I_m (b_m - X_m y_{m-1} - Y_m y_{m+1})
+            if (lane < 9) Xb[lane] = rv;
+            wave_sync();
+            if (lane < 9) vb[j * 9 + lane] = dot9(A + lane * 9, Xb);
+        } else if (lane < 9) {
+            vb[j * 9 + lane] = rv;
+        }
+    }
     wave_sync();
 }
 
 // the two ends (threads 0..127: wave 0 top blocks 0..m-1, wave 1 bottom blocks NB-1..m+1)
-template <typename T> __device__ void tw_factor_ends(T *Sd, T *So, int NB, int m, LdsT<T> *sh) {
+template <typename T> __device__ void tw_factor_ends(T *Sd, T *So, int NB, int m, LdsT<T> *sh, LdsT<T> *vb) {
     const int lane = threadIdx.x & 63;
     const int e0 = lane, e1 = lane + 64;
     const bool has1 = e1 < 81;
@@ -798,7 +827,8 @@ template <typename T> __device__ void tw_factor_ends(T *Sd, T *So, int NB, int m
         fetch(So + (size_t)(top ? 0 : NB - 2) * 81, p0, p1);
         fetch(Sd + (size_t)(j0 + dj) * 81, n0, n1);
     }
-    tw_step<T>(d0, d1, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, Sd + (size_t)j0 * 81, A, P, Xb, Dd);
+    tw_step<T>(d0, d1, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, Sd + (size_t)j0 * 81, A, P, Xb, Dd, vb,
+               j0);
     for (int s = 1, j = j0 + dj; s < nstep; ++s, j += dj) {
         Ob[e0] = p0;
         if (has1) Ob[e1] = p1;
@@ -811,16 +841,16 @@ template <typename T> __device__ void tw_factor_ends(T *Sd, T *So, int NB, int m
         }
         if (top)
             tw_step<T>(d0, d1, Ob, P, nullptr, nullptr, So + (size_t)(j - 1) * 81, nullptr, Sd + (size_t)j * 81, A,
-                       P, Xb, Dd);
+                       P, Xb, Dd, vb, j, j - 1, 0);
         else
             tw_step<T>(d0, d1, nullptr, nullptr, Ob, P, nullptr, So + (size_t)j * 81, Sd + (size_t)j * 81, A, P,
-                       Xb, Dd);
+                       Xb, Dd, vb, j, 0, j + 1);
     }
 }
 
 // the meeting block (wave 0, after a workgroup barrier): I_{m-1} and I_{m+1} are the two waves'
 // previous inverses in LDS
-template <typename T> __device__ void tw_factor_meet(T *Sd, T *So, int m, LdsT<T> *sh) {
+template <typename T> __device__ void tw_factor_meet(T *Sd, T *So, int m, LdsT<T> *sh, LdsT<T> *vb) {
     const int lane = threadIdx.x & 63;
     const int e0 = lane, e1 = lane + 64;
     const bool has1 = e1 < 81;
@@ -832,7 +862,7 @@ template <typename T> __device__ void tw_factor_meet(T *Sd, T *So, int m, LdsT<T
     const T d0 = Sd[(size_t)m * 81 + e0], d1 = has1 ? Sd[(size_t)m * 81 + e1] : T(0);
     wave_sync();
     tw_step<T>(d0, d1, Op, P, Oq, Pq, So + (size_t)(m - 1) * 81, So + (size_t)m * 81, Sd + (size_t)m * 81, A, P,
-               Xb, Dd);
+               Xb, Dd, vb, m, m - 1, m + 1);
 }
 
 // Chunked, double-buffered stream of 9x9 blocks from the workspace into per-wave LDS: each sweep
@@ -1091,7 +1121,7 @@ __device__ __forceinline__ T dz_rows(const Ctx<T, ROBOT> &C, int k, const T (&dx
                                      const int ld, const T *__restrict__ st, const T *__restrict__ fu,
                                      const T *__restrict__ rdu, const T *__restrict__ rdi,
                                      const T *__restrict__ sv, const T *__restrict__ lm, T *__restrict__ ds,
-                                     T *__restrict__ dl) {
+                                     T *__restrict__ dl, T (&mus)[3]) {
     using S = Stage<ROBOT>;
     using R_ = Rows<ROBOT>;
     constexpr int NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
@@ -1102,8 +1132,13 @@ __device__ __forceinline__ T dz_rows(const Ctx<T, ROBOT> &C, int k, const T (&dx
         const T dsr = pr ? -rdi[r * ld] - g : T(0);
         ds[r * ld] = dsr;
         dl[r * ld] = dlr;
+        const T sr = sv[r * ld], lr = lm[r * ld];
+        // sum_r (s + a ds)(lambda + a dl) = mus0 + a mus1 + a^2 mus2 (absent rows: lambda = ds = dl = 0)
+        mus[0] = fma(sr, lr, mus[0]);
+        mus[1] = fma(sr, dlr, fma(lr, dsr, mus[1]));
+        mus[2] = fma(dsr, dlr, mus[2]);
         // branch-free ratio tests (selects keep the row loop one basic block)
-        const T qs = fdiv(-sv[r * ld], dsr < T(0) ? dsr : T(-1)), ql = fdiv(-lm[r * ld], dlr < T(0) ? dlr : T(-1));
+        const T qs = fdiv(-sr, dsr < T(0) ? dsr : T(-1)), ql = fdiv(-lr, dlr < T(0) ? dlr : T(-1));
         amax = fmin(amax, fmin(dsr < T(0) ? qs : T(1), dlr < T(0) ? ql : T(1)));
     };
 #pragma unroll
@@ -1145,7 +1180,7 @@ __device__ __forceinline__ T dz_rows(const Ctx<T, ROBOT> &C, int k, const T (&dx
 }
 
 template <typename T, int ROBOT>
-__device__ PHASE_ATTR T phase_dz(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu) {
+__device__ PHASE_ATTR T phase_dz(const Ctx<T, ROBOT> &C, int k, int corr, T (&mus)[3]) {
     using S = Stage<ROBOT>;
     using R_ = Rows<ROBOT>;
     constexpr int NI = R_::NI;
@@ -1182,20 +1217,11 @@ __device__ PHASE_ATTR T phase_dz(const Ctx<T, ROBOT> &C, int k, int corr, T sigm
     const T amax = dz_rows<T, ROBOT>(C, k, dx, dtt, du, eu, dlt, dls, rh, ld, C.stage + kc,
                                      C.ws + WF(facu) * KPC + kc, C.ws + WF(rdu) * KPC + kc, C.ws + WF(rdi) * KPC + k,
                                      C.ws + WF(s) * KPC + k, C.ws + WF(l) * KPC + k, C.ws + (corr ? WF(ds) : WF(dsa)) * KPC + k,
-                                     C.ws + (corr ? WF(dl) : WF(dla)) * KPC + k);
+                                     C.ws + (corr ? WF(dl) : WF(dla)) * KPC + k, mus);
     stv(C.kv(WF(dx), k), dx);
     C.kv(WF(dt), k)[0] = dtt;
     if (hu) stv(C.kv(WF(du), k), du);
     return amax;
-}
-
-template <typename T, int ROBOT> __device__ T mu_after(const Ctx<T, ROBOT> &C, int k, T a) {
-    constexpr int NI = Rows<ROBOT>::NI;
-    const SV<T> s = C.kv(WF(s), k), lm = C.kv(WF(l), k), ds = C.kv(WF(dsa), k), dl = C.kv(WF(dla), k);
-    T acc = T(0);
-    for (int r = 0; r < NI; ++r)
-        acc += (s[r] + a * ds[r]) * (lm[r] + a * dl[r]);   // absent rows: lambda = dl = 0
-    return acc;
 }
 
 // z, nu, s, lambda += a * direction (dnu from the LDS vector)
@@ -1264,7 +1290,7 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_init_shift(con
 
 // ------------------------------------------------------------------ kernel
 template <typename T, int ROBOT>
-__global__ void __launch_bounds__(NT) k_qp_ipm(DevBuf<T> d, int only_active, int max_iter, T eps_abs, T eps_rel,
+__global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int only_active, int max_iter, T eps_abs, T eps_rel,
                                                T eta) {
     extern __shared__ __attribute__((aligned(16))) unsigned char dsmem[];
     constexpr int NI = Rows<ROBOT>::NI;
@@ -1352,45 +1378,54 @@ __global__ void __launch_bounds__(NT) k_qp_ipm(DevBuf<T> d, int only_active, int
             if (stall >= 3 && merit <= T(1e3)) { status = 1; break; }
         }
         if (it == max_iter) break;
-        // ---- factorization
-        for (int k = tid; k < K1; k += NT) phase_factor<T, ROBOT>(C, k);
+        // ---- Phi factors and the predictor's particular solution (knot-local), then the S blocks
+        // and the predictor's Schur right-hand side
+        for (int k = tid; k < K1; k += NT) {
+            phase_factor<T, ROBOT>(C, k);
+            phase_w<T, ROBOT>(C, k, 0, T(0));
+        }
         __syncthreads();
         STAMP(1);
-        for (int k = tid; k < K1; k += NT) phase_sblock<T, ROBOT>(C, k);
+        for (int k = tid; k < K1; k += NT) {
+            phase_sblock<T, ROBOT>(C, k);
+            phase_rhs<T, ROBOT>(C, k);
+        }
         __syncthreads();
         STAMP(2);
-        if (tid < 128) tw_factor_ends<T>(C.Sd, C.So, NB, NBm, shl);
+        // ---- factorization of S with the predictor's forward elimination fused in
+        if (tid < 128) tw_factor_ends<T>(C.Sd, C.So, NB, NBm, shl, C.vb);
         __syncthreads();
-        if (tid < 64) tw_factor_meet<T>(C.Sd, C.So, NBm, shl);
+        if (tid < 64) tw_factor_meet<T>(C.Sd, C.So, NBm, shl, C.vb);
+        __syncthreads();
         STAMP(3);
-        __syncthreads();
         // ---- predictor (affine) and corrector
         T sigma_mu = T(0);
         T alpha = T(1);
         for (int corr = 0; corr < 2; ++corr) {
-            for (int k = tid; k < K1; k += NT) phase_w<T, ROBOT>(C, k, corr, sigma_mu);
-            __syncthreads();
-            STAMP(4);
-            for (int k = tid; k < K1; k += NT) phase_rhs<T, ROBOT>(C, k);
-            __syncthreads();
-            STAMP(5);
-            if (tid < 128) tw_solve_elim<T>(C.So, NB, NBm, C.vb, ring);
-            __syncthreads();
-            if (tid < 64) tw_solve_meet<T>(C.Sd, C.So, NB, NBm, C.vb, shl);
-            __syncthreads();
+            if (corr) {
+                for (int k = tid; k < K1; k += NT) phase_w<T, ROBOT>(C, k, corr, sigma_mu);
+                __syncthreads();
+                STAMP(4);
+                for (int k = tid; k < K1; k += NT) phase_rhs<T, ROBOT>(C, k);
+                __syncthreads();
+                STAMP(5);
+                if (tid < 128) tw_solve_elim<T>(C.So, NB, NBm, C.vb, ring);
+                __syncthreads();
+                if (tid < 64) tw_solve_meet<T>(C.Sd, C.So, NB, NBm, C.vb, shl);
+                __syncthreads();
+            }
             if (tid < 128) tw_solve_back<T>(C.Sd, C.So, NB, NBm, C.vb, ring);
+            __syncthreads();
             STAMP(6);
-            T am[1] = {T(1)};
-            for (int k = tid; k < K1; k += NT) am[0] = fmin(am[0], phase_dz<T, ROBOT>(C, k, corr, sigma_mu));
+            T am[1] = {T(1)}, mus[3] = {T(0), T(0), T(0)};
+            for (int k = tid; k < K1; k += NT) am[0] = fmin(am[0], phase_dz<T, ROBOT>(C, k, corr, mus));
             block_reduce<T, NT, 1, 2>(am, red);
             STAMP(7);
             alpha = am[0];
             if (init) break;
-            if (corr == 0) {
-                T ma[1] = {T(0)};
-                for (int k = tid; k < K1; k += NT) ma[0] += mu_after<T, ROBOT>(C, k, alpha);
-                block_reduce<T, NT, 1, 0>(ma, red);
-                const T mu_aff = ma[0] / fmax(sm2[1], T(1));
+            if (corr == 0) {   // Mehrotra centering from the affine step's complementarity
+                block_reduce<T, NT, 3, 0>(mus, red);
+                const T mu_aff = (mus[0] + alpha * (mus[1] + alpha * mus[2])) / fmax(sm2[1], T(1));
                 const T sg = mu_aff / fmax(mu, T(1e-300));
                 sigma_mu = sg * sg * sg * mu;
             }

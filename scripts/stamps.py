@@ -14,7 +14,7 @@ s = Solver(pb.robot, N, B, 'fp64'); s.upload(pb)
 s.scp_iterate(True); s.synchronize()
 s.timing_begin(); s.scp_iterate(True); t = s.timing_end()
 st = s.debug_stamps().astype(float)
-names = ['residual', 'factor', 'sblock', 'seq_factor', 'phase_w', 'rhs', 'seq_solve', 'dz', 'update']
+names = ['residual', 'factor+w_pred', 'sblock+rhs_pred', 'seq_factor+elim', 'w_corr', 'rhs_corr', 'seq_solve', 'dz', 'update']
 its = s.qp_iterations_total() / B
 tot = st[:, :9].sum(axis=1).mean()
 print('B', B, 'N', N, 'qp_ms', t['qp_ms'], 'ipm iters', its, 'cycles/problem %.3g' % tot)
