@@ -713,7 +713,7 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_sblock(const C
 // are fetched one step ahead (a step is thousands of cycles).  Inverses by Gauss-Jordan sweeps
 // over the 64 lanes (SPD: no pivoting) with a pivot floor relative to the original diagonal
 // (near the solution of a degenerate QP the Schur blocks are differences of O(M) numbers).
-// Per-wave LDS scratch: A (current) | P (previous inverse) | Xb | Ob | Dd (original diagonal).
+// Per-wave LDS scratch: A (current) | P (previous inverse) | Xb | Ob | Dd (original diagonal) | Dn (S_jj).
 template <typename T> __device__ __forceinline__ T dot9(const LdsT<T> *a, const LdsT<T> *b) {
     T av[9], bv[9];
 #pragma unroll
@@ -723,54 +723,63 @@ template <typename T> __device__ __forceinline__ T dot9(const LdsT<T> *a, const 
     for (int q = 3; q < 9; q += 3) { s0 = fma(av[q], bv[q], s0); s1 = fma(av[q + 1], bv[q + 1], s1); s2 = fma(av[q + 2], bv[q + 2], s2); }
     return s0 + s1 + s2;
 }
-constexpr int TW_SCRATCH = 4 * 88 + 16;
+constexpr int TW_SCRATCH = 5 * 88 + 16;
 
 // With vb != nullptr the step also runs the forward elimination of the right-hand side held in
 // vb (the predictor's, known before the factorization): y_j = b_j - X_j y_jx (top), or
 // b_j - Y_j y_jy (bottom), or at the meeting block x_m = I_m (b_m - X_m y_{m-1} - Y_m y_{m+1}),
 // with X_j / Y_j read from the LDS scratch while they are there.
 template <typename T>
-__device__ __forceinline__ void tw_step(T d0, T d1, const LdsT<T> *Op, const LdsT<T> *Ip, const LdsT<T> *Oq,
+__device__ __forceinline__ void tw_step(const LdsT<T> *Dn, const LdsT<T> *Op, const LdsT<T> *Ip, const LdsT<T> *Oq,
                                         const LdsT<T> *Iq, T *Xout, T *Yout, T *Iout, LdsT<T> *A, LdsT<T> *P,
                                         LdsT<T> *Xb, LdsT<T> *Dd, LdsT<T> *vb = nullptr, int j = 0, int jx = 0,
-                                        int jy = 0) {
+                                        int jy = 0, unsigned long long *sub = nullptr) {
+#ifdef CMPC_STAMPS
+    unsigned long long tq = __builtin_amdgcn_s_memtime();
+#define SUBSTAMP(i) do { if (sub) { const unsigned long long tn = __builtin_amdgcn_s_memtime(); sub[i] += tn - tq; tq = tn; } } while (0)
+#else
+#define SUBSTAMP(i) do { } while (0)
+#endif
     const int lane = threadIdx.x & 63;
     const int e0 = lane, e1 = lane + 64;
     const bool has1 = e1 < 81;
     const int i0 = e0 / 9, c0 = e0 % 9, i1 = e1 / 9, c1 = e1 % 9;
+    const T d0 = Dn[e0], d1 = has1 ? Dn[e1] : T(0);
     T a0 = d0, a1 = d1;
     T rv = (vb && lane < 9) ? vb[j * 9 + lane] : T(0);   // b_j (fused elimination)
     if (e0 % 10 == 0) Dd[e0 / 10] = d0;
     if (e1 == 80) Dd[8] = d1;
     T x0 = T(0), x1 = T(0), y0 = T(0), y1 = T(0);
+    // 9-term dot products with every LDS operand read before the first multiply
+    auto dot = [&](auto fa, auto fb) -> T {
+        T u[9], v[9];
+#pragma unroll
+        for (int m = 0; m < 9; ++m) { u[m] = fa(m); v[m] = fb(m); }
+        T s0 = u[0] * v[0], s1 = u[1] * v[1], s2 = u[2] * v[2];
+#pragma unroll
+        for (int m = 3; m < 9; m += 3) { s0 = fma(u[m], v[m], s0); s1 = fma(u[m + 1], v[m + 1], s1); s2 = fma(u[m + 2], v[m + 2], s2); }
+        return s0 + s1 + s2;
+    };
     if (Op) {   // X = Op' I_{j-1};  A -= X Op   (Op = S_{j-1,j})
-        for (int m = 0; m < 9; ++m) {
-            x0 = fma(Op[m * 9 + i0], Ip[m * 9 + c0], x0);
-            if (has1) x1 = fma(Op[m * 9 + i1], Ip[m * 9 + c1], x1);
-        }
+        x0 = dot([&](int m) { return Op[m * 9 + i0]; }, [&](int m) { return Ip[m * 9 + c0]; });
+        if (has1) x1 = dot([&](int m) { return Op[m * 9 + i1]; }, [&](int m) { return Ip[m * 9 + c1]; });
         Xb[e0] = x0;
         if (has1) Xb[e1] = x1;
         wave_sync();
         if (vb && lane < 9) rv -= dot9(Xb + lane * 9, vb + jx * 9);
-        for (int m = 0; m < 9; ++m) {
-            a0 = fma(-Xb[i0 * 9 + m], Op[m * 9 + c0], a0);
-            if (has1) a1 = fma(-Xb[i1 * 9 + m], Op[m * 9 + c1], a1);
-        }
+        a0 -= dot([&](int m) { return Xb[i0 * 9 + m]; }, [&](int m) { return Op[m * 9 + c0]; });
+        if (has1) a1 -= dot([&](int m) { return Xb[i1 * 9 + m]; }, [&](int m) { return Op[m * 9 + c1]; });
         wave_sync();
     }
     if (Oq) {   // Y = Oq I_{j+1};  A -= Y Oq'   (Oq = S_{j,j+1})
-        for (int m = 0; m < 9; ++m) {
-            y0 = fma(Oq[i0 * 9 + m], Iq[m * 9 + c0], y0);
-            if (has1) y1 = fma(Oq[i1 * 9 + m], Iq[m * 9 + c1], y1);
-        }
+        y0 = dot([&](int m) { return Oq[i0 * 9 + m]; }, [&](int m) { return Iq[m * 9 + c0]; });
+        if (has1) y1 = dot([&](int m) { return Oq[i1 * 9 + m]; }, [&](int m) { return Iq[m * 9 + c1]; });
         Xb[e0] = y0;
         if (has1) Xb[e1] = y1;
         wave_sync();
         if (vb && lane < 9) rv -= dot9(Xb + lane * 9, vb + jy * 9);
-        for (int m = 0; m < 9; ++m) {
-            a0 = fma(-Xb[i0 * 9 + m], Oq[c0 * 9 + m], a0);
-            if (has1) a1 = fma(-Xb[i1 * 9 + m], Oq[c1 * 9 + m], a1);
-        }
+        a0 -= dot([&](int m) { return Xb[i0 * 9 + m]; }, [&](int m) { return Oq[c0 * 9 + m]; });
+        if (has1) a1 -= dot([&](int m) { return Xb[i1 * 9 + m]; }, [&](int m) { return Oq[c1 * 9 + m]; });
         wave_sync();
     }
     A[e0] = a0;
@@ -778,23 +787,34 @@ __device__ __forceinline__ void tw_step(T d0, T d1, const LdsT<T> *Op, const Lds
     if (Op) { Xout[e0] = x0; if (has1) Xout[e1] = x1; }
     if (Oq) { Yout[e0] = y0; if (has1) Yout[e1] = y1; }
     wave_sync();
+    SUBSTAMP(0);
+    // Gauss-Jordan, branch-free, with the next pivot's reciprocal computed one pivot ahead: every
+    // lane forms A'_{c+1,c+1} = A_{c+1,c+1} - (A_{c+1,c} / p_c) A_{c,c+1} (the same expression the
+    // owning lane stores) from broadcast reads, so its reciprocal chain overlaps the update
+    T ip = rcp_nr(fmax(A[0], T(1e-13) * Dd[0]));
+#pragma unroll
     for (int c = 0; c < 9; ++c) {
-        const T p = fmax(A[c * 9 + c], T(1e-13) * Dd[c]);
-        const T ip = rcp_nr(p);
-        const T aic0 = A[i0 * 9 + c], acj0 = A[c * 9 + c0], aij0 = A[e0];
-        T aic1 = T(0), acj1 = T(0), aij1 = T(0);
-        if (has1) { aic1 = A[i1 * 9 + c]; acj1 = A[c * 9 + c1]; aij1 = A[e1]; }
-        wave_sync();
+        const T aic0 = A[i0 * 9 + c], acj0 = A[c * 9 + c0];
+        const T aic1 = A[(has1 ? i1 : 0) * 9 + c], acj1 = A[c * 9 + (has1 ? c1 : 0)];
+        T ipn = T(0);
+        if (c < 8) {
+            const T ncc = A[(c + 1) * 9 + c + 1], nic = A[(c + 1) * 9 + c], nci = A[c * 9 + c + 1];
+            ipn = rcp_nr(fmax(fma(-(nic * ip), nci, ncc), T(1e-13) * Dd[c + 1]));
+        }
         auto upd = [&](int i, int cc, T aic, T acj, T aij) -> T {
-            if (i != c && cc != c) return fma(-aic * ip, acj, aij);
-            if (i == c && cc != c) return acj * ip;
-            if (i != c && cc == c) return -aic * ip;
-            return ip;
+            const T mi = aic * ip;
+            const T gen = fma(-mi, acj, aij), row = acj * ip, col = -mi;
+            return i == c ? (cc == c ? ip : row) : (cc == c ? col : gen);
         };
-        A[e0] = upd(i0, c0, aic0, acj0, aij0);
-        if (has1) A[e1] = upd(i1, c1, aic1, acj1, aij1);
+        a0 = upd(i0, c0, aic0, acj0, a0);
+        a1 = upd(i1, c1, aic1, acj1, a1);
         wave_sync();
+        A[e0] = a0;
+        if (has1) A[e1] = a1;
+        wave_sync();
+        ip = ipn;
     }
+    SUBSTAMP(1);
     const T r0 = A[e0], r1 = has1 ? A[e1] : T(0);
     P[e0] = r0;
     if (has1) P[e1] = r1;
@@ -810,42 +830,57 @@ __device__ __forceinline__ void tw_step(T d0, T d1, const LdsT<T> *Op, const Lds
         }
     }
     wave_sync();
+    SUBSTAMP(2);
+#undef SUBSTAMP
 }
 
-// the two ends (threads 0..127: wave 0 top blocks 0..m-1, wave 1 bottom blocks NB-1..m+1)
-template <typename T> __device__ void tw_factor_ends(T *Sd, T *So, int NB, int m, LdsT<T> *sh, LdsT<T> *vb) {
+// the two ends (threads 0..127: wave 0 top blocks 0..m-1, wave 1 bottom blocks NB-1..m+1).  The
+// raw blocks of step s + 1 are loaded during step s and landed in LDS at its end, inside the same
+// loop iteration: registers carried over the back-edge with loads in flight would make the
+// compiler drain the whole memory queue (this step's stores included) at the loop header.
+template <typename T>
+__device__ void tw_factor_ends(T *Sd, T *So, int NB, int m, LdsT<T> *sh, LdsT<T> *vb, unsigned long long *stamp_out) {
     const int lane = threadIdx.x & 63;
     const int e0 = lane, e1 = lane + 64;
     const bool has1 = e1 < 81;
     const bool top = (threadIdx.x >> 6) == 0;
-    LdsT<T> *A = sh + (top ? 0 : TW_SCRATCH), *P = A + 88, *Xb = A + 176, *Ob = A + 264, *Dd = A + 352;
-    T p0 = T(0), p1 = T(0), d0, d1, n0 = T(0), n1 = T(0);
-    auto fetch = [&](const T *blk, T &v0, T &v1) { v0 = blk[e0]; v1 = blk[has1 ? e1 : 80]; };
+    LdsT<T> *A = sh + (top ? 0 : TW_SCRATCH), *P = A + 88, *Xb = A + 176, *Ob = A + 264, *Dd = A + 352,
+            *Dn = A + 368;
     const int j0 = top ? 0 : NB - 1, dj = top ? 1 : -1, nstep = top ? m : NB - 1 - m;
-    fetch(Sd + (size_t)j0 * 81, d0, d1);
-    if (nstep > 1) {
-        fetch(So + (size_t)(top ? 0 : NB - 2) * 81, p0, p1);
-        fetch(Sd + (size_t)(j0 + dj) * 81, n0, n1);
+    auto land = [&](LdsT<T> *dst, T v0, T v1) { dst[e0] = v0; if (has1) dst[e1] = v1; };
+    unsigned long long sub[4] = {0, 0, 0, 0};
+    unsigned long long *subp = stamp_out ? sub : nullptr;
+    {
+        const T *D0 = Sd + (size_t)j0 * 81;
+        land(Dn, D0[e0], D0[has1 ? e1 : 80]);
     }
-    tw_step<T>(d0, d1, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, Sd + (size_t)j0 * 81, A, P, Xb, Dd, vb,
-               j0);
-    for (int s = 1, j = j0 + dj; s < nstep; ++s, j += dj) {
-        Ob[e0] = p0;
-        if (has1) Ob[e1] = p1;
-        d0 = n0;
-        d1 = n1;
-        wave_sync();
-        if (s + 1 < nstep) {   // raw blocks of the next step
-            fetch(So + (size_t)(top ? j : j - 1) * 81, p0, p1);
-            fetch(Sd + (size_t)(j + dj) * 81, n0, n1);
-        }
-        if (top)
-            tw_step<T>(d0, d1, Ob, P, nullptr, nullptr, So + (size_t)(j - 1) * 81, nullptr, Sd + (size_t)j * 81, A,
-                       P, Xb, Dd, vb, j, j - 1, 0);
+    wave_sync();
+    for (int s = 0, j = j0; s < nstep; ++s, j += dj) {
+        // raw blocks of the next step (clamped past the end: branch-free loads)
+        const int jn = s + 1 < nstep ? j + dj : j;
+        const T *On = So + (size_t)(top ? jn - 1 : jn) * 81, *Dnx = Sd + (size_t)jn * 81;
+        const T p0 = On[e0], p1 = On[has1 ? e1 : 80], n0 = Dnx[e0], n1 = Dnx[has1 ? e1 : 80];
+        if (s == 0)
+            tw_step<T>(Dn, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, Sd + (size_t)j * 81, A, P, Xb, Dd,
+                       vb, j, 0, 0, subp);
+        else if (top)
+            tw_step<T>(Dn, Ob, P, nullptr, nullptr, So + (size_t)(j - 1) * 81, nullptr, Sd + (size_t)j * 81, A, P,
+                       Xb, Dd, vb, j, j - 1, 0, subp);
         else
-            tw_step<T>(d0, d1, nullptr, nullptr, Ob, P, nullptr, So + (size_t)j * 81, Sd + (size_t)j * 81, A, P,
-                       Xb, Dd, vb, j, 0, j + 1);
+            tw_step<T>(Dn, nullptr, nullptr, Ob, P, nullptr, So + (size_t)j * 81, Sd + (size_t)j * 81, A, P, Xb,
+                       Dd, vb, j, 0, j + 1, subp);
+#ifdef CMPC_STAMPS
+        const unsigned long long tl = __builtin_amdgcn_s_memtime();
+#endif
+        land(Ob, p0, p1);
+        land(Dn, n0, n1);
+        wave_sync();
+#ifdef CMPC_STAMPS
+        sub[3] += __builtin_amdgcn_s_memtime() - tl;
+#endif
     }
+    if (stamp_out && lane == 0 && top)
+        for (int i = 0; i < 4; ++i) stamp_out[12 + i] += sub[i];
 }
 
 // the meeting block (wave 0, after a workgroup barrier): I_{m-1} and I_{m+1} are the two waves'
@@ -859,9 +894,11 @@ template <typename T> __device__ void tw_factor_meet(T *Sd, T *So, int m, LdsT<T
     Op[e0] = So[(size_t)(m - 1) * 81 + e0];
     Oq[e0] = So[(size_t)m * 81 + e0];
     if (has1) { Op[e1] = So[(size_t)(m - 1) * 81 + e1]; Oq[e1] = So[(size_t)m * 81 + e1]; }
-    const T d0 = Sd[(size_t)m * 81 + e0], d1 = has1 ? Sd[(size_t)m * 81 + e1] : T(0);
+    LdsT<T> *Dn = A + 368;
+    Dn[e0] = Sd[(size_t)m * 81 + e0];
+    if (has1) Dn[e1] = Sd[(size_t)m * 81 + e1];
     wave_sync();
-    tw_step<T>(d0, d1, Op, P, Oq, Pq, So + (size_t)(m - 1) * 81, So + (size_t)m * 81, Sd + (size_t)m * 81, A, P,
+    tw_step<T>(Dn, Op, P, Oq, Pq, So + (size_t)(m - 1) * 81, So + (size_t)m * 81, Sd + (size_t)m * 81, A, P,
                Xb, Dd, vb, m, m - 1, m + 1);
 }
 
@@ -1393,7 +1430,11 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
         __syncthreads();
         STAMP(2);
         // ---- factorization of S with the predictor's forward elimination fused in
-        if (tid < 128) tw_factor_ends<T>(C.Sd, C.So, NB, NBm, shl, C.vb);
+#ifdef CMPC_STAMPS
+        if (tid < 128) tw_factor_ends<T>(C.Sd, C.So, NB, NBm, shl, C.vb, d.stamps + (size_t)b * 16);
+#else
+        if (tid < 128) tw_factor_ends<T>(C.Sd, C.So, NB, NBm, shl, C.vb, nullptr);
+#endif
         __syncthreads();
         if (tid < 64) tw_factor_meet<T>(C.Sd, C.So, NBm, shl, C.vb);
         __syncthreads();
@@ -1463,7 +1504,7 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
         d.qp_status[b] = status;
         d.qp_iters[b] = it;
 #ifdef CMPC_STAMPS
-        for (int i = 0; i < 12; ++i) d.stamps[(size_t)b * 16 + i] = t_acc[i];
+        for (int i = 0; i < 12; ++i) d.stamps[(size_t)b * 16 + i] = t_acc[i];   // 12..15: tw_factor_ends sub-steps
 #endif
     }
 #undef STAMP

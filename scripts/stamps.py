@@ -20,3 +20,7 @@ tot = st[:, :9].sum(axis=1).mean()
 print('B', B, 'N', N, 'qp_ms', t['qp_ms'], 'ipm iters', its, 'cycles/problem %.3g' % tot)
 for i, n in enumerate(names):
     print('  %-11s %5.1f%%  %.3g cycles/IPM-iter' % (n, 100 * st[:, i].mean() / tot, st[:, i].mean() / its))
+# tw_factor_ends sub-steps (top wave; accumulated over the warm-up and the timed iteration)
+sub = st[:, 12:16].mean(axis=0) / 2.0
+nst = its * (N + 2) // 2
+print('  factor step sub-phases (cycles/step): X+A %.0f  GJ %.0f  tail %.0f  land %.0f' % tuple(sub / nst))
