@@ -1,0 +1,50 @@
+"""Summarize rocprofv3 PMC passes (FETCH_SIZE and WRITE_SIZE, separate runs) into per-launch HBM
+bytes of the QP kernel -> profiles/qp_pmc_traffic.json (read by bench.py's roofline.traffic).
+
+FETCH_SIZE is doubled per MI355X_MICROARCH.md (gfx950 reports half the bytes of wide reads);
+both counters are in KB.  Usage: python scripts/pmc_traffic.py <fetch_dir> <write_dir> [out]
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def per_kernel(d, counter):
+    f = glob.glob(os.path.join(d, '**', '*counter_collection.csv'), recursive=True)[0]
+    tot, n = collections.defaultdict(float), collections.defaultdict(set)
+    for r in csv.DictReader(open(f)):
+        if r['Counter_Name'] != counter:
+            continue
+        name = r['Kernel_Name'].split('(')[0]
+        tot[name] += float(r['Counter_Value'])
+        n[name].add(r['Dispatch_Id'])
+    return {k: (tot[k], len(n[k])) for k in tot}
+
+
+def main():
+    fdir, wdir = sys.argv[1], sys.argv[2]
+    out = sys.argv[3] if len(sys.argv) > 3 else os.path.join(os.path.dirname(__file__), '..', 'profiles',
+                                                              'qp_pmc_traffic.json')
+    fe, wr = per_kernel(fdir, 'FETCH_SIZE'), per_kernel(wdir, 'WRITE_SIZE')
+    qp = [k for k in fe if 'k_qp_ipm' in k][0]
+    fkb, fn = fe[qp]
+    wkb, wn = wr[qp]
+    per_launch = (2.0 * fkb / fn + wkb / wn) * 1024.0
+    res = {'source': 'rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), python3 bench.py --steps 2 '
+                     '--warmup 0 --no-cpu-baseline',
+           'kernel': qp, 'dispatches': {'FETCH_SIZE': fn, 'WRITE_SIZE': wn},
+           'fetch_size_kb_per_launch': fkb / fn, 'write_size_kb_per_launch': wkb / wn,
+           'correction': 'FETCH_SIZE x2 (MI355X_MICROARCH.md: gfx950 FETCH_SIZE reports half of the bytes of wide '
+                         'reads); counters in KB',
+           'hbm_bytes_per_launch': per_launch,
+           'per_kernel_kb_per_launch': {c: {k: v[0] / v[1] for k, v in d.items()} for c, d in
+                                        (('FETCH_SIZE', fe), ('WRITE_SIZE', wr))}}
+    json.dump(res, open(out, 'w'), indent=1)
+    print(json.dumps({'kernel': qp, 'hbm_bytes_per_launch': per_launch}))
+
+
+if __name__ == '__main__':
+    main()
