@@ -15,67 +15,89 @@
 
 namespace cmpc {
 
-// C[m x n] = op(A) * op(B) with lanes over output entries; row-major LDS operands.
-// ta: A stored as (k x m) and used transposed; tb: B stored as (n x k) and used transposed.
-template <typename T>
-__device__ __forceinline__ void wmm(T *Cm, const T *Am, const T *Bm, int m, int n, int k, bool ta, bool tb,
-                                    int lane, T beta_c = T(0), const T *Cadd = nullptr, T alpha = T(1)) {
-    for (int e = lane; e < m * n; e += WAVE) {
-        const int i = e / n, j = e % n;
-        T acc = T(0);
-        for (int q = 0; q < k; ++q) {
-            const T a = ta ? Am[q * m + i] : Am[i * k + q];
-            const T b = tb ? Bm[j * k + q] : Bm[q * n + j];
-            acc = fma(a, b, acc);
+// C[M x N] = alpha op(A) op(B) (+ Cadd) with lanes over output entries; row-major LDS operands.
+// TA: A stored as (K x M) and used transposed; TB: B stored as (N x K) and used transposed.  The
+// dimensions are compile-time so every lane's K operands are read before its multiply chain.
+template <int M, int N, int K, bool TA, bool TB, typename T>
+__device__ __forceinline__ void wmm(T *Cm, const T *Am, const T *Bm, int lane, const T *Cadd = nullptr,
+                                    T alpha = T(1)) {
+#pragma unroll
+    for (int e0 = 0; e0 < M * N; e0 += WAVE) {
+        const int e = e0 + lane;
+        if (e < M * N) {
+            const int i = e / N, j = e % N;
+            T a[K], bb[K];
+#pragma unroll
+            for (int q = 0; q < K; ++q) {
+                a[q] = TA ? Am[q * M + i] : Am[i * K + q];
+                bb[q] = TB ? Bm[j * K + q] : Bm[q * N + j];
+            }
+            T s0 = T(0), s1 = T(0);
+#pragma unroll
+            for (int q = 0; q < K; q += 2) {
+                s0 = fma(a[q], bb[q], s0);
+                if (q + 1 < K) s1 = fma(a[q + 1], bb[q + 1], s1);
+            }
+            T v = alpha * (s0 + s1);
+            if (Cadd) v += Cadd[e];
+            Cm[e] = v;
         }
-        T v = alpha * acc;
-        if (Cadd) v += Cadd[e];
-        else if (beta_c != T(0)) v += beta_c * Cm[e];   // never read an uninitialized C when beta = 0
-        Cm[e] = v;
     }
     wave_sync();
 }
 
-// In-place Cholesky (lower) of an SPD n x n LDS matrix; the strict upper part is left stale.
-template <typename T> __device__ void wchol(T *M, int n, int lane) {
+template <typename T> __device__ __forceinline__ T lin_rcp(T p) {
+    T r;
+    if constexpr (sizeof(T) == 8) r = __builtin_amdgcn_rcp(p); else r = __builtin_amdgcn_rcpf(p);
+    r = fma(r, fma(-p, r, T(1)), r);
+    return fma(r, fma(-p, r, T(1)), r);
+}
+
+// In-place inverse of an SPD n x n LDS matrix by Gauss-Jordan over the lanes (no pivoting; the
+// LQR matrix R + B'PB is SPD with R > 0), branch-free, the next pivot's reciprocal formed one
+// pivot ahead from broadcast reads so its chain overlaps the update.
+template <int n, typename T> __device__ __forceinline__ void wgj_inv(T *M, int lane) {
+    constexpr int E = (n * n + WAVE - 1) / WAVE;
+    T a[E];
+    int ii[E], jj[E];
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        const int e = lane + r * WAVE;
+        ii[r] = e < n * n ? e / n : n;
+        jj[r] = e < n * n ? e % n : n;
+        a[r] = e < n * n ? M[e] : T(0);
+    }
+    T ip = lin_rcp(M[0]);
+#pragma unroll
     for (int c = 0; c < n; ++c) {
-        const T d = sqrt(M[c * n + c]);
-        const T id = T(1) / d;
-        wave_sync();
-        for (int i = c + 1 + lane; i < n; i += WAVE) M[i * n + c] *= id;
-        if (lane == 0) M[c * n + c] = d;
-        wave_sync();
-        const int rem = n - c - 1;
-        for (int e = lane; e < rem * rem; e += WAVE) {
-            const int i = c + 1 + e / rem, j = c + 1 + e % rem;
-            if (j <= i) M[i * n + j] -= M[i * n + c] * M[j * n + c];
+        T aic[E], acj[E];
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+            aic[r] = M[(ii[r] < n ? ii[r] : 0) * n + c];
+            acj[r] = M[c * n + (jj[r] < n ? jj[r] : 0)];
+        }
+        T ipn = T(0);
+        if (c + 1 < n) ipn = lin_rcp(fma(-(M[(c + 1) * n + c] * ip), M[c * n + c + 1], M[(c + 1) * n + c + 1]));
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+            const T mi = aic[r] * ip;
+            const T gen = fma(-mi, acj[r], a[r]), row = acj[r] * ip, col = -mi;
+            a[r] = ii[r] == c ? (jj[r] == c ? ip : row) : (jj[r] == c ? col : gen);
         }
         wave_sync();
+#pragma unroll
+        for (int r = 0; r < E; ++r)
+            if (lane + r * WAVE < n * n) M[lane + r * WAVE] = a[r];
+        wave_sync();
+        ip = ipn;
     }
-}
-
-// X (n x r, row-major) <- M^-1 X for the Cholesky factor L (lower) in M; lanes over columns.
-template <typename T> __device__ void wchol_solve(const T *L, T *X, int n, int r, int lane) {
-    for (int j = lane; j < r; j += WAVE) {
-        for (int i = 0; i < n; ++i) {          // forward  L y = x
-            T s = X[i * r + j];
-            for (int q = 0; q < i; ++q) s -= L[i * n + q] * X[q * r + j];
-            X[i * r + j] = s / L[i * n + i];
-        }
-        for (int i = n - 1; i >= 0; --i) {     // backward L' z = y
-            T s = X[i * r + j];
-            for (int q = i + 1; q < n; ++q) s -= L[q * n + i] * X[q * r + j];
-            X[i * r + j] = s / L[i * n + i];
-        }
-    }
-    wave_sync();
 }
 
 template <typename T, int ROBOT> struct LinSmem {
     static constexpr int NC = Robot<ROBOT>::NC;
     T x[9], u[NU], p[3 * NC], R[9 * NC], a[NC];
     T A[81], Bm[9 * NU], Cm[9 * 3 * NC];
-    T P[81], AtP[81], AtPA[81], PB[9 * NU], AtPB[9 * NU], M[NU * NU], X[NU * 9], tmp[9 * 3 * NC];
+    T P[81], AtP[81], AtPA[81], PB[9 * NU], AtPB[9 * NU], M[NU * NU], X[NU * 9];   // PB doubles as C W scratch
 };
 
 template <typename T, int ROBOT>
@@ -184,24 +206,19 @@ __device__ void linearize_knot(const DevBuf<T> &d, const DevParams<T> &prm, int 
     for (int e = lane; e < 81; e += WAVE) s.P[e] = prm.Q[e];
     wave_sync();
     // ---- LQR: two Riccati steps from P = Q, then K   (src/centroidal_model.py:217-228)
+    //   X = (R + B'PB)^-1 B'PA (Gauss-Jordan inverse over the lanes), P = Q + A'PA - A'PB X
     for (int it = 0; it < 3; ++it) {
-        wmm(s.AtP, s.A, s.P, 9, 9, 9, true, false, lane);            // A' P
-        wmm(s.PB, s.P, s.Bm, 9, NU, 9, false, false, lane);          // P B
-        wmm(s.M, s.Bm, s.PB, NU, NU, 9, true, false, lane, T(0), prm.R);   // R + B' P B
-        wmm(s.AtPB, s.AtP, s.Bm, 9, NU, 9, false, false, lane);      // A' P B
-        if (it < 2) wmm(s.AtPA, s.AtP, s.A, 9, 9, 9, false, false, lane);
-        wchol(s.M, NU, lane);
-        for (int e = lane; e < NU * 9; e += WAVE) s.X[e] = s.AtPB[(e % 9) * NU + e / 9];   // (A'PB)' = B'PA
-        wave_sync();
-        wchol_solve(s.M, s.X, NU, 9, lane);                           // (R + B'PB)^-1 B'PA
+        wmm<9, 9, 9, true, false>(s.AtP, s.A, s.P, lane);            // A' P
+        wmm<9, NU, 9, false, false>(s.PB, s.P, s.Bm, lane);          // P B
+        wmm<NU, NU, 9, true, false>(s.M, s.Bm, s.PB, lane, prm.R);   // R + B' P B
+        wmm<9, NU, 9, false, false>(s.AtPB, s.AtP, s.Bm, lane);      // A' P B
+        if (it < 2) wmm<9, 9, 9, false, false>(s.AtPA, s.AtP, s.A, lane);
+        wgj_inv<NU>(s.M, lane);
+        wmm<NU, 9, NU, false, true>(s.X, s.M, s.AtPB, lane);         // (R + B'PB)^-1 (A'PB)'
         if (it < 2) {
             // P = Q + A'PA - A'PB X
-            for (int e = lane; e < 81; e += WAVE) {
-                const int i = e / 9, j = e % 9;
-                T acc = T(0);
-                for (int q = 0; q < NU; ++q) acc = fma(s.AtPB[i * NU + q], s.X[q * 9 + j], acc);
-                s.P[e] = prm.Q[e] + s.AtPA[e] - acc;
-            }
+            wmm<9, 9, NU, false, false>(s.P, s.AtPB, s.X, lane, s.AtPA, T(-1));
+            for (int e = lane; e < 81; e += WAVE) s.P[e] += prm.Q[e];
             wave_sync();
         }
     }
@@ -213,66 +230,128 @@ __device__ void linearize_knot(const DevBuf<T> &d, const DevParams<T> &prm, int 
         for (int q = 0; q < NU; ++q) acc -= s.Bm[i * NU + q] * s.X[q * 9 + j];
         d.Acl[kn * 81 + e] = acc;
     }
+    static_assert(9 * NW <= 9 * NU, "C W scratch");
+    T *cw = s.PB;
     for (int e = lane; e < 9 * NW; e += WAVE) {
         const int i = e / NW, j = e % NW;
         T acc = T(0);
         for (int q = 0; q < NW; ++q) acc = fma(s.Cm[i * NW + q], prm.cov_w[q * NW + j], acc);
-        s.tmp[e] = acc;
+        cw[e] = acc;
     }
     wave_sync();
     for (int e = lane; e < 81; e += WAVE) {
         const int i = e / 9, j = e % 9;
         T acc = prm.cov_eta[e];
-        for (int q = 0; q < NW; ++q) acc = fma(s.tmp[i * NW + q], s.Cm[j * NW + q], acc);
+        for (int q = 0; q < NW; ++q) acc = fma(cw[i * NW + q], s.Cm[j * NW + q], acc);
         d.Qw[kn * 81 + e] = acc;
     }
     wave_sync();
 }
 
+// Covariance scan (src/centroidal_model.py:234-238, 266, 284), wave 0 of the workgroup after all
+// knots are linearized: Sigma_{k+1} = Acl_k Sigma_k Acl_k' + Qw_k.  The per-step blocks stream
+// through the (then dead) per-knot LDS scratch in double-buffered chunks of KS steps, each
+// chunk's loads issued a chunk ahead inside one loop iteration (no in-flight registers over the
+// back-edge), so the 100-step chain runs out of LDS.
+constexpr int KS = 4;
 template <typename T, int ROBOT>
-__global__ void __launch_bounds__(256) k_linearize(DevBuf<T> d, int only_active) {
+__global__ void __launch_bounds__(256, 4) k_linearize(DevBuf<T> d, int only_active) {
     const int b = blockIdx.x;
     if (b >= d.B) return;
     if (only_active && !d.scp[b].active) return;
+    // four per-wave scratch records (under 40 KB at fp64: four workgroups per CU)
     __shared__ LinSmem<T, ROBOT> sm[4];
-    __shared__ T S[81], Tm[81];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const DevParams<T> &prm = d.params[d.class_id[b]];
     const int N = d.N;
+#ifdef CMPC_STAMPS
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
     for (int k = wid; k < N; k += 4) linearize_knot<T, ROBOT>(d, prm, b, k, sm[wid], lane);
+#ifdef CMPC_STAMPS
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+#endif
     __syncthreads();
     __threadfence_block();
     if (wid != 0) return;
-    // ---- covariance scan (src/centroidal_model.py:234-238, 266, 284)
+    constexpr int CH = 2 * KS * 81;                          // one chunk: KS Acl + KS Qw blocks
+    constexpr int PL = (CH + WAVE - 1) / WAVE;
+    static_assert(2 * CH * sizeof(T) <= 3 * sizeof(LinSmem<T, ROBOT>), "scan chunk buffers");
+    T *buf = reinterpret_cast<T *>(&sm[1]);
+    T *S = sm[0].P, *Tm = sm[0].AtP;
+    const T *Acl = d.Acl + (size_t)b * N * 81, *Qw = d.Qw + (size_t)b * N * 81;
+    T reg[PL];
+    auto issue = [&](int c) {
+#pragma unroll
+        for (int r = 0; r < PL; ++r) {
+            const int e = min(lane + r * WAVE, CH - 1), blk = e / 81, w = e % 81;
+            const int k = min(c * KS + blk % KS, N - 1);
+            reg[r] = (blk < KS ? Acl : Qw)[(size_t)k * 81 + w];
+        }
+    };
+    auto land = [&](int c) {
+        T *dst = buf + (c & 1) * CH;
+#pragma unroll
+        for (int r = 0; r < PL; ++r)
+            if (lane + r * WAVE < CH) dst[lane + r * WAVE] = reg[r];
+    };
     for (int e = lane; e < 81; e += WAVE) {
         S[e] = T(0);
         d.Sig[((size_t)b * (N + 1)) * 81 + e] = T(0);
     }
+    issue(0);
+    land(0);
     wave_sync();
-    for (int k = 0; k < N; ++k) {
-        const T *Ac = d.Acl + ((size_t)b * N + k) * 81;
-        const T *Qw = d.Qw + ((size_t)b * N + k) * 81;
-        for (int e = lane; e < 81; e += WAVE) {     // Tm = Acl S
-            const int i = e / 9, j = e % 9;
-            T acc = T(0);
-            for (int q = 0; q < 9; ++q) acc = fma(Ac[i * 9 + q], S[q * 9 + j], acc);
-            Tm[e] = acc;
+    for (int c = 0; c * KS < N; ++c) {
+        issue(c + 1);
+        const T *cb = buf + (c & 1) * CH;
+        for (int q = 0; q < KS; ++q) {
+            const int k = c * KS + q;
+            if (k >= N) break;
+            const T *Ac = cb + q * 81, *Q = cb + (KS + q) * 81;
+            for (int e = lane; e < 81; e += WAVE) {     // Tm = Acl S
+                const int i = e / 9, j = e % 9;
+                T a[9], sv[9];
+#pragma unroll
+                for (int m = 0; m < 9; ++m) { a[m] = Ac[i * 9 + m]; sv[m] = S[m * 9 + j]; }
+                T acc = T(0);
+#pragma unroll
+                for (int m = 0; m < 9; ++m) acc = fma(a[m], sv[m], acc);
+                Tm[e] = acc;
+            }
+            wave_sync();
+            T out[2];
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {   // Tm Acl' + Qw
+                const int e = min(lane + r * WAVE, 80), i = e / 9, j = e % 9;
+                T t[9], a[9];
+#pragma unroll
+                for (int m = 0; m < 9; ++m) { t[m] = Tm[i * 9 + m]; a[m] = Ac[j * 9 + m]; }
+                T acc = Q[e];
+#pragma unroll
+                for (int m = 0; m < 9; ++m) acc = fma(t[m], a[m], acc);
+                out[r] = acc;
+            }
+            wave_sync();
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const int e = lane + r * WAVE;
+                if (e < 81) {
+                    S[e] = out[r];
+                    d.Sig[((size_t)b * (N + 1) + k + 1) * 81 + e] = out[r];
+                }
+            }
+            wave_sync();
         }
-        wave_sync();
-        T out[2];
-        for (int r = 0, e = lane; e < 81; e += WAVE, ++r) {   // Tm Acl' + Qw
-            const int i = e / 9, j = e % 9;
-            T acc = Qw[e];
-            for (int q = 0; q < 9; ++q) acc = fma(Tm[i * 9 + q], Ac[j * 9 + q], acc);
-            out[r] = acc;
-        }
-        wave_sync();
-        for (int r = 0, e = lane; e < 81; e += WAVE, ++r) {
-            S[e] = out[r];
-            d.Sig[((size_t)b * (N + 1) + k + 1) * 81 + e] = out[r];
-        }
+        land(c + 1);
         wave_sync();
     }
+#ifdef CMPC_STAMPS
+    if (lane == 0) {
+        d.stamps[(size_t)b * 16 + 9] = t1 - t0;
+        d.stamps[(size_t)b * 16 + 10] = __builtin_amdgcn_s_memtime() - t1;
+    }
+#endif
 }
 
 template __global__ void k_linearize<double, 0>(DevBuf<double>, int);

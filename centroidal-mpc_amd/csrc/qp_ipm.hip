@@ -1504,7 +1504,7 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
         d.qp_status[b] = status;
         d.qp_iters[b] = it;
 #ifdef CMPC_STAMPS
-        for (int i = 0; i < 12; ++i) d.stamps[(size_t)b * 16 + i] = t_acc[i];   // 12..15: tw_factor_ends sub-steps
+        for (int i = 0; i < 9; ++i) d.stamps[(size_t)b * 16 + i] = t_acc[i];   // 9..11: k_linearize, 12..15: tw_factor_ends
 #endif
     }
 #undef STAMP

@@ -24,3 +24,5 @@ for i, n in enumerate(names):
 sub = st[:, 12:16].mean(axis=0) / 2.0
 nst = its * (N + 2) // 2
 print('  factor step sub-phases (cycles/step): X+A %.0f  GJ %.0f  tail %.0f  land %.0f' % tuple(sub / nst))
+lin = st[:, 9:11].mean(axis=0)
+print('  k_linearize per problem: knots (wave 0) %.3g cycles, covariance scan %.3g cycles' % tuple(lin))
