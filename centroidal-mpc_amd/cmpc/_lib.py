@@ -51,7 +51,9 @@ EXPORTS = ['cmpc_create', 'cmpc_destroy', 'cmpc_last_error', 'cmpc_version', 'cm
            'cmpc_qp_solve', 'cmpc_accept', 'cmpc_scp_iterate', 'cmpc_solve_scp', 'cmpc_synchronize',
            'cmpc_get_linearization', 'cmpc_qp_sizes', 'cmpc_export_qp', 'cmpc_get_qp_solution',
            'cmpc_get_solution', 'cmpc_get_iteration_log', 'cmpc_get_timing', 'cmpc_timing_begin',
-           'cmpc_timing_end', 'cmpc_get_qp_iterations_total', 'cmpc_debug_stamps']
+           'cmpc_timing_end', 'cmpc_get_qp_iterations_total', 'cmpc_debug_stamps', 'cmpc_set_scp_mode',
+           'cmpc_get_linearization_point', 'cmpc_interpolate']
+SCP_MODE = {'reference': 0, 'gusto': 1}
 
 _lib = None
 
@@ -98,6 +100,9 @@ def load():
         'cmpc_timing_end': (i32, [h, P(Timing), P(ctypes.c_int)]),
         'cmpc_get_qp_iterations_total': (i32, [h, P(ctypes.c_int64)]),
         'cmpc_debug_stamps': (i32, [h, vp]),
+        'cmpc_set_scp_mode': (i32, [h, i32]),
+        'cmpc_get_linearization_point': (i32, [h, vp, vp, vp]),
+        'cmpc_interpolate': (i32, [h, i32, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -239,6 +244,24 @@ class Solver:
 
     def synchronize(self):
         self._chk(self.lib.cmpc_synchronize(self.h), 'cmpc_synchronize')
+
+    def set_scp_mode(self, mode):
+        """'reference' (default: quirk Q1, the linearization point stays at the warm start) or
+        'gusto' (accepted solutions become the next linearization point; include/cmpc.h)."""
+        self._chk(self.lib.cmpc_set_scp_mode(self.h, SCP_MODE[mode]), 'cmpc_set_scp_mode')
+
+    def linearization_point(self):
+        X = np.zeros((self.B, self.N + 1, 9)); U = np.zeros((self.B, self.N, 12)); conv = np.zeros(self.B)
+        self._chk(self.lib.cmpc_get_linearization_point(self.h, _ptr(X), _ptr(U), _ptr(conv)),
+                  'cmpc_get_linearization_point')
+        return X, U, conv
+
+    def interpolate(self, n_inner=10):
+        """Device interpolate_SCP_solution of every problem's accepted solution:
+        X (B, 9, N*n_inner), U (B, 12, (N-1)*n_inner)."""
+        X = np.zeros((self.B, 9, self.N * n_inner)); U = np.zeros((self.B, 12, (self.N - 1) * n_inner))
+        self._chk(self.lib.cmpc_interpolate(self.h, int(n_inner), _ptr(X), _ptr(U)), 'cmpc_interpolate')
+        return X, U
 
     # ---- getters
     def linearization(self):

@@ -31,17 +31,18 @@ __global__ void __launch_bounds__(128) k_assemble(DevBuf<T> d, int only_active) 
     if (only_active && !sc.active) return;
     const DevParams<T> &prm = d.params[d.class_id[b]];
     const SV<T> st{d.stage + (size_t)b * St::SIZE * KPC + k};   // field-major record (common.hpp)
-    const T *xb = d.Xbar + gid * 9;
+    const T *xr = d.Xbar + gid * 9;   // warm start: tracking reference (src/cost.py:21-29)
+    const T *xb = d.Xlin + gid * 9;   // linearization point (= warm start in reference mode, quirk Q1)
     const T radius = T(sc.radius);
     if (k == 0) d.cw[b] = T(-1.0 / sc.weight);
-    for (int i = 0; i < 9; ++i) st[St::QX + i] = prm.tracking ? -prm.Wx[i] * xb[i] : T(0);
+    for (int i = 0; i < 9; ++i) st[St::QX + i] = prm.tracking ? -prm.Wx[i] * xr[i] : T(0);
     for (int j = 0; j < 8; ++j) {
         const T s0 = (j & 1) ? T(-1) : T(1), s1 = (j & 2) ? T(-1) : T(1), s2 = (j & 4) ? T(-1) : T(1);
         st[St::BTR + j] = radius + (s0 * xb[6] + s1 * xb[7] + s2 * xb[8]);
     }
     if (k == N) return;
     const size_t kn = (size_t)b * N + k;
-    const T *A = d.A + kn * 81, *Bm = d.Bu + kn * 9 * NU, *f = d.f + kn * 9, *ub = d.Ubar + kn * NU;
+    const T *A = d.A + kn * 81, *Bm = d.Bu + kn * 9 * NU, *f = d.f + kn * 9, *ub = d.Ulin + kn * NU;
     for (int i = 0; i < 9; ++i) {
         T acc = -f[i];
         for (int j = 0; j < 9; ++j) acc = fma(A[i * 9 + j], xb[j], acc);

@@ -18,6 +18,7 @@ namespace cmpc {
 template <typename T, int R> __global__ void k_linearize(DevBuf<T>, int);
 template <typename T, int R> __global__ void k_assemble(DevBuf<T>, int);
 template <typename T, int R> __global__ void k_qp_ipm(DevBuf<T>, int, int, T, T, T);
+template <typename T> __global__ void k_interpolate(DevBuf<T>, int, int, T *, T *);
 size_t ipm_lds_bytes(int N, int prec_bytes);
 template <typename T, int R> __global__ void k_accept(DevBuf<T>, int);
 template <typename T, int R> __global__ void k_rollout(DevBuf<T>, const T *, const T *, T *);
@@ -95,7 +96,9 @@ struct cmpc_handle_s {
          *Ubar = nullptr, *f = nullptr, *A = nullptr, *Bu = nullptr, *C = nullptr, *K = nullptr, *Sig = nullptr,
          *Acl = nullptr, *Qw = nullptr, *stage = nullptr, *cw = nullptr, *xs = nullptr, *us = nullptr, *ts = nullptr,
          *nus = nullptr, *lams = nullptr, *qp_status = nullptr, *qp_iters = nullptr, *ws = nullptr, *scp = nullptr,
-         *Xacc = nullptr, *Uacc = nullptr, *Kacc = nullptr, *Sacc = nullptr, *stamps = nullptr;
+         *Xacc = nullptr, *Uacc = nullptr, *Kacc = nullptr, *Sacc = nullptr, *stamps = nullptr, *Xlin = nullptr,
+         *Ulin = nullptr;
+    int scp_mode = CMPC_SCP_MODE_REFERENCE;
 
     size_t esz() const { return prec == CMPC_PREC_F64 ? 8 : 4; }
     void *dalloc(size_t bytes) {
@@ -111,6 +114,7 @@ struct cmpc_handle_s {
         d.class_id = (const int32_t *)class_id; d.params = (const DevParams<T> *)params;
         d.logic = (const uint8_t *)logic; d.pos = (const T *)pos; d.rot = (const T *)rot;
         d.Xbar = (const T *)Xbar; d.Ubar = (const T *)Ubar;
+        d.Xlin = (T *)Xlin; d.Ulin = (T *)Ulin; d.scp_mode = scp_mode;
         d.f = (T *)f; d.A = (T *)A; d.Bu = (T *)Bu; d.C = (T *)C; d.K = (T *)K; d.Sig = (T *)Sig;
         d.Acl = (T *)Acl; d.Qw = (T *)Qw; d.stage = (T *)stage; d.cw = (T *)cw;
         d.xs = (T *)xs; d.us = (T *)us; d.ts = (T *)ts; d.nus = (T *)nus; d.lams = (T *)lams;
@@ -224,6 +228,23 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
     HIPCHK(hipGetLastError());
 }
 
+template <typename T> void interpolate_impl(cmpc_handle h, int ni, double *Xo, double *Uo) {
+    const size_t B = h->B, N = h->N, nx = B * 9 * N * ni, nuo = B * NU * (N - 1) * ni;
+    void *dX = nullptr, *dU = nullptr;
+    HIPCHK(hipMalloc(&dX, nx * sizeof(T)));
+    HIPCHK(hipMalloc(&dU, std::max<size_t>(nuo, 1) * sizeof(T)));
+    struct Free {
+        void *p[2];
+        ~Free() { for (void *q : p) if (q) (void)hipFree(q); }
+    } fr{{dX, dU}};
+    const long n = (long)(nx + nuo);
+    hipLaunchKernelGGL((k_interpolate<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream, h->buf<T>(),
+                       ni, (int)NU, (T *)dX, (T *)dU);
+    HIPCHK(hipGetLastError());
+    from_dev<T>(h, Xo, dX, nx);
+    from_dev<T>(h, Uo, dU, nuo);
+}
+
 template <typename T, int R> void rollout_impl(cmpc_handle h, const double *X, const double *U, double *out) {
     const size_t nx = (size_t)h->B * (h->N + 1) * 9, nu = (size_t)h->B * h->N * NU;
     void *dX = nullptr, *dU = nullptr, *dO = nullptr;
@@ -315,6 +336,8 @@ int cmpc_create(cmpc_handle *out, int device, int robot, int N, int max_batch, i
         h->rot = h->dalloc(Bm * N * NC * 9 * e);
         h->Xbar = h->dalloc(Bm * K1 * 9 * e);
         h->Ubar = h->dalloc(Bm * N * NU * e);
+        h->Xlin = h->dalloc(Bm * K1 * 9 * e);
+        h->Ulin = h->dalloc(Bm * N * NU * e);
         h->f = h->dalloc(Bm * N * 9 * e);
         h->A = h->dalloc(Bm * N * 81 * e);
         h->Bu = h->dalloc(Bm * N * 9 * NU * e);
@@ -427,6 +450,9 @@ int cmpc_upload(cmpc_handle h, int B, const int32_t *class_id, const int8_t *log
         up(h->rot, rot, (size_t)B * N * NC * 9);
         up(h->Xbar, Xbar, (size_t)B * (N + 1) * 9);
         up(h->Ubar, Ubar, (size_t)B * N * NU);
+        // the linearization point starts at the warm start
+        HIPCHK(hipMemcpyAsync(h->Xlin, h->Xbar, (size_t)B * (N + 1) * 9 * h->esz(), hipMemcpyDeviceToDevice, h->stream));
+        HIPCHK(hipMemcpyAsync(h->Ulin, h->Ubar, (size_t)B * N * NU * h->esz(), hipMemcpyDeviceToDevice, h->stream));
         reset_scp(h, class_id);
     });
 }
@@ -441,6 +467,38 @@ int cmpc_set_trust_region(cmpc_handle h, const double *weight, const double *rad
         }
         HIPCHK(hipMemcpyAsync(h->scp, st.data(), st.size() * sizeof(ScpState), hipMemcpyHostToDevice, h->stream));
         HIPCHK(hipStreamSynchronize(h->stream));
+    });
+}
+
+int cmpc_set_scp_mode(cmpc_handle h, int mode) {
+    return guard(h, [&] {
+        need(mode == CMPC_SCP_MODE_REFERENCE || mode == CMPC_SCP_MODE_GUSTO, "unknown SCP mode");
+        h->scp_mode = mode;
+    });
+}
+
+int cmpc_get_linearization_point(cmpc_handle h, double *X, double *U, double *convergence) {
+    return guard(h, [&] {
+        need(h->B > 0, "no problems uploaded");
+        const size_t B = h->B, N = h->N;
+        auto dl = [&](double *dst, void *src, size_t n) {
+            if (h->prec == CMPC_PREC_F64) from_dev<double>(h, dst, src, n); else from_dev<float>(h, dst, src, n);
+        };
+        dl(X, h->Xlin, B * (N + 1) * 9);
+        dl(U, h->Ulin, B * N * NU);
+        if (convergence) {
+            auto st = get_scp(h);
+            for (size_t b = 0; b < B; ++b) convergence[b] = st[b].conv;
+        }
+    });
+}
+
+int cmpc_interpolate(cmpc_handle h, int n_inner, double *X_out, double *U_out) {
+    return guard(h, [&] {
+        need(h->B > 0, "no problems uploaded");
+        need(n_inner >= 1 && X_out && U_out, "invalid interpolation arguments");
+        if (h->prec == CMPC_PREC_F64) interpolate_impl<double>(h, n_inner, X_out, U_out);
+        else interpolate_impl<float>(h, n_inner, X_out, U_out);
     });
 }
 

@@ -56,6 +56,7 @@ struct ScpState {
     double tr_norm, rho;
     int iter, status, success, n_accepted;
     int qp_status, qp_iters, decision, active;
+    double conv;   // convergence measure of the last accepted iteration (GuSTO mode)
 };
 
 // Device buffers of one handle.
@@ -65,7 +66,9 @@ template <typename T> struct DevBuf {
     const DevParams<T> *params;
     const uint8_t *logic;    // (B,N,NC)
     const T *pos, *rot;      // (B,N,NC,3) (B,N,NC,9)
-    const T *Xbar, *Ubar;    // (B,N+1,9) (B,N,NU)
+    const T *Xbar, *Ubar;    // (B,N+1,9) (B,N,NU) warm start: tracking reference, boundary states
+    T *Xlin, *Ulin;          // (B,N+1,9) (B,N,NU) linearization point (= warm start in reference mode)
+    int scp_mode;            // CMPC_SCP_MODE_*
     // linearization
     T *f, *A, *Bu, *C, *K, *Sig;    // (B,N,9) (B,N,81) (B,N,108) (B,N,9*3NC) (B,N,108) (B,N+1,81)
     T *Acl, *Qw;                    // scan helpers (B,N,81) x2

@@ -108,8 +108,8 @@ __device__ void linearize_knot(const DevBuf<T> &d, const DevParams<T> &prm, int 
     const int N = d.N;
     const size_t kn = (size_t)b * N + k;
     // ---- stage inputs
-    if (lane < 9) s.x[lane] = d.Xbar[((size_t)b * (N + 1) + k) * 9 + lane];
-    if (lane < NU) s.u[lane] = d.Ubar[kn * NU + lane];
+    if (lane < 9) s.x[lane] = d.Xlin[((size_t)b * (N + 1) + k) * 9 + lane];   // linearization point
+    if (lane < NU) s.u[lane] = d.Ulin[kn * NU + lane];
     if (lane < 3 * NC) s.p[lane] = d.pos[kn * 3 * NC + lane];
     if (lane < 9 * NC) s.R[lane] = d.rot[kn * 9 * NC + lane];
     if (lane < NC) s.a[lane] = T(d.logic[kn * NC + lane]);

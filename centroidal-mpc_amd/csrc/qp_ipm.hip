@@ -747,8 +747,10 @@ __device__ __forceinline__ void tw_step(const LdsT<T> *Dn, const LdsT<T> *Op, co
     const T d0 = Dn[e0], d1 = has1 ? Dn[e1] : T(0);
     T a0 = d0, a1 = d1;
     T rv = (vb && lane < 9) ? vb[j * 9 + lane] : T(0);   // b_j (fused elimination)
+    // original diagonal of S_jj (pivot floor): entries 0, 10, ..., 60 are lanes' first elements,
+    // 70 and 80 second elements
     if (e0 % 10 == 0) Dd[e0 / 10] = d0;
-    if (e1 == 80) Dd[8] = d1;
+    if (has1 && e1 % 10 == 0) Dd[e1 / 10] = d1;
     T x0 = T(0), x1 = T(0), y0 = T(0), y1 = T(0);
     // 9-term dot products with every LDS operand read before the first multiply
     auto dot = [&](auto fa, auto fb) -> T {
@@ -1367,12 +1369,13 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
 #else
 #define STAMP(i) do { } while (0)
 #endif
-    // ---- starting point of the initialization step: z = (xbar, ubar, 0), nu = 0, s = lambda = 1
+    // ---- starting point of the initialization step: z = (xlin, ulin, 0), nu = 0, s = lambda = 1
     for (int k = tid; k < K1; k += NT) {
         const SV<T> x = C.var_x(k);
-        for (int i = 0; i < 9; ++i) x[i] = C.xbar[(size_t)k * 9 + i];
+        const T *xl = d.Xlin + ((size_t)b * K1 + k) * 9;   // start at the linearization point
+        for (int i = 0; i < 9; ++i) x[i] = xl[i];
         C.kv(WF(t), k)[0] = T(0);
-        const T *ubar = d.Ubar + ((size_t)b * N + (k < N ? k : 0)) * NU;
+        const T *ubar = d.Ulin + ((size_t)b * N + (k < N ? k : 0)) * NU;
         if (k < N) { const SV<T> u = C.var_u(k); for (int i = 0; i < NU; ++i) u[i] = ubar[i]; }
         const SV<T> s = C.kv(WF(s), k), lm = C.kv(WF(l), k), dsa = C.kv(WF(dsa), k), dla = C.kv(WF(dla), k);
         const unsigned msk = C.cmask(k);

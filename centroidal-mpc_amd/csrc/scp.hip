@@ -15,28 +15,28 @@ namespace cmpc {
 
 enum { DEC_NONE = 0, DEC_ACCEPT = 1, DEC_REJECT_RHO = 2, DEC_REJECT_TR = 3, DEC_QP_FAILED = -1 };
 
-__device__ double jacobi_lambda_max(double (&a)[9][9]) {
+template <int n> __device__ double jacobi_lambda_max(double (&a)[n][n]) {
     for (int sweep = 0; sweep < 40; ++sweep) {
         double off = 0.0, tot = 0.0;
-        for (int i = 0; i < 9; ++i)
-            for (int j = 0; j < 9; ++j) {
+        for (int i = 0; i < n; ++i)
+            for (int j = 0; j < n; ++j) {
                 tot += a[i][j] * a[i][j];
                 if (i != j) off += a[i][j] * a[i][j];
             }
         if (off <= 1e-30 * tot || off == 0.0) break;
-        for (int p = 0; p < 8; ++p)
-            for (int q = p + 1; q < 9; ++q) {
+        for (int p = 0; p < n - 1; ++p)
+            for (int q = p + 1; q < n; ++q) {
                 const double apq = a[p][q];
                 if (apq == 0.0) continue;
                 const double theta = (a[q][q] - a[p][p]) / (2.0 * apq);
                 const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
                 const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
-                for (int k = 0; k < 9; ++k) {
+                for (int k = 0; k < n; ++k) {
                     const double akp = a[k][p], akq = a[k][q];
                     a[k][p] = c * akp - s * akq;
                     a[k][q] = s * akp + c * akq;
                 }
-                for (int k = 0; k < 9; ++k) {
+                for (int k = 0; k < n; ++k) {
                     const double apk = a[p][k], aqk = a[q][k];
                     a[p][k] = c * apk - s * aqk;
                     a[q][k] = s * apk + c * aqk;
@@ -44,8 +44,34 @@ __device__ double jacobi_lambda_max(double (&a)[9][9]) {
             }
     }
     double m = a[0][0];
-    for (int i = 1; i < 9; ++i) m = fmax(m, a[i][i]);
+    for (int i = 1; i < n; ++i) m = fmax(m, a[i][i]);
     return m;
+}
+
+// Spectral norm of the (rows x cols) matrix V[c][r] - W[c][r] (W may be null): sqrt of the largest
+// eigenvalue of the rows x rows Gram matrix, accumulated over the workgroup (Gram entry per
+// thread), Jacobi on thread 0.  All threads receive the value.
+template <int rows, typename T>
+__device__ double spec_norm(const T *V, const T *W, int cols, double *gram, double *res) {
+    const int tid = threadIdx.x;
+    if (tid < rows * rows) {
+        const int i = tid / rows, j = tid % rows;
+        double g = 0.0;
+        for (int c = 0; c < cols; ++c) {
+            const double vi = double(V[(size_t)c * rows + i]) - (W ? double(W[(size_t)c * rows + i]) : 0.0);
+            const double vj = double(V[(size_t)c * rows + j]) - (W ? double(W[(size_t)c * rows + j]) : 0.0);
+            g += vi * vj;
+        }
+        gram[tid] = g;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        double a[rows][rows];
+        for (int e = 0; e < rows * rows; ++e) a[e / rows][e % rows] = gram[e];
+        *res = sqrt(fmax(jacobi_lambda_max<rows>(a), 0.0));
+    }
+    __syncthreads();
+    return *res;
 }
 
 // x+ = x + dt F(x, u) for the knot-k contact data (integrate_model_one_step)
@@ -82,12 +108,13 @@ __global__ void __launch_bounds__(256) k_accept(DevBuf<T> d, int fixed_iters) {
     ScpState &sc = d.scp[b];
     if (!sc.active) return;
     __shared__ T red[2 * 4];
-    __shared__ double gram[81];
+    __shared__ double gram[NU * NU], nres[4];
     __shared__ int dec_sh;
     const int tid = threadIdx.x, N = d.N, K1 = N + 1;
     const DevParams<T> &prm = d.params[d.class_id[b]];
     const T *Xs = d.xs + (size_t)b * K1 * 9, *Us = d.us + (size_t)b * N * NU;
-    const T *Xb = d.Xbar + (size_t)b * K1 * 9, *Ub = d.Ubar + (size_t)b * N * NU;
+    // previous solution = the linearization point (the warm start in reference mode, quirk Q1)
+    T *Xb = d.Xlin + (size_t)b * K1 * 9, *Ub = d.Ulin + (size_t)b * N * NU;
     const int qst = d.qp_status[b];
     // ---- rho (fp of the compute type)
     T acc[2] = {T(0), T(0)};
@@ -110,20 +137,18 @@ __global__ void __launch_bounds__(256) k_accept(DevBuf<T> d, int fixed_iters) {
     }
     block_reduce<T, 256, 2, 0>(acc, red);
     const double rho = double(acc[0]) / double(acc[1]);
-    // ---- Gram matrix of X_sol - Xbar (double)
-    if (tid < 81) {
-        const int i = tid / 9, j = tid % 9;
-        double g = 0.0;
-        for (int k = 0; k < K1; ++k)
-            g += (double(Xs[(size_t)k * 9 + i]) - double(Xb[(size_t)k * 9 + i])) *
-                 (double(Xs[(size_t)k * 9 + j]) - double(Xb[(size_t)k * 9 + j]));
-        gram[tid] = g;
+    // ---- spectral norm of X_sol - X_prev (quirk Q6)
+    const double tr = spec_norm<9>(Xs, Xb, K1, gram, &nres[0]);
+    // ---- GuSTO mode: convergence(sol, lin) = |dU|_2 / |U|_2 + |dX|_2 / |X|_2 (src/scp_solver.py:51-56),
+    // needed only when this iteration is accepted (evaluated for every problem, cheap)
+    double conv = 0.0;
+    if (d.scp_mode == CMPC_SCP_MODE_GUSTO) {
+        const double nx = spec_norm<9>(Xs, (const T *)nullptr, K1, gram, &nres[1]);
+        const double nu_d = spec_norm<NU>(Us, Ub, N, gram, &nres[2]);
+        const double nu_n = spec_norm<NU>(Us, (const T *)nullptr, N, gram, &nres[3]);
+        conv = nu_d / nu_n + tr / nx;
     }
-    __syncthreads();
     if (tid == 0) {
-        double a[9][9];
-        for (int e = 0; e < 81; ++e) a[e / 9][e % 9] = gram[e];
-        const double tr = sqrt(fmax(jacobi_lambda_max(a), 0.0));
         int dec;
         sc.qp_status = qst;
         sc.qp_iters = d.qp_iters[b];
@@ -154,13 +179,18 @@ __global__ void __launch_bounds__(256) k_accept(DevBuf<T> d, int fixed_iters) {
             sc.status = CMPC_SCP_QP_FAILED;
             if (!fixed_iters) sc.active = 0;
         } else if (!fixed_iters) {
-            const bool cont = sc.iter < prm.max_iterations && sc.weight < prm.omega_max && !(sc.iter != 0 && sc.success);
+            // loop condition of src/scp_solver.py:132-133; reference mode: convergence == 0 (Q1)
+            if (dec == DEC_ACCEPT) sc.conv = conv;
+            const bool conv_ok = d.scp_mode == CMPC_SCP_MODE_GUSTO ? sc.conv < prm.conv_thr : 0.0 < prm.conv_thr;
+            const bool cont = sc.iter < prm.max_iterations && sc.weight < prm.omega_max &&
+                              !(sc.iter != 0 && sc.success && conv_ok);
             if (!cont) {
                 sc.active = 0;
                 sc.status = sc.success ? CMPC_SCP_CONVERGED : CMPC_SCP_MAX_ITER;
             }
-        } else if (sc.status == CMPC_SCP_RUNNING && sc.success) {
-            sc.status = CMPC_SCP_CONVERGED;
+        } else {
+            if (dec == DEC_ACCEPT) sc.conv = conv;
+            if (sc.status == CMPC_SCP_RUNNING && sc.success) sc.status = CMPC_SCP_CONVERGED;
         }
         dec_sh = dec;
     }
@@ -171,7 +201,38 @@ __global__ void __launch_bounds__(256) k_accept(DevBuf<T> d, int fixed_iters) {
     for (int e = tid; e < N * NU; e += 256) d.Uacc[(size_t)b * N * NU + e] = Us[e];
     for (int e = tid; e < N * NU * 9; e += 256) d.Kacc[(size_t)b * N * NU * 9 + e] = d.K[(size_t)b * N * NU * 9 + e];
     for (int e = tid; e < K1 * 81; e += 256) d.Sacc[(size_t)b * K1 * 81 + e] = d.Sig[(size_t)b * K1 * 81 + e];
+    if (d.scp_mode == CMPC_SCP_MODE_GUSTO) {   // the accepted solution becomes the linearization point
+        for (int e = tid; e < K1 * 9; e += 256) Xb[e] = Xs[e];
+        for (int e = tid; e < N * NU; e += 256) Ub[e] = Us[e];
+    }
 }
+
+// interpolate_SCP_solution (src/scp_solver.py:95-111) of the accepted solution, one thread per
+// (problem, output column, row): column i * ni + j = v_i + j * ((v_{i+1} - v_i) / ni).
+// X_out (B, 9, N * ni), U_out (B, nu, (N - 1) * ni), nu = nu_out (reference control width).
+template <typename T>
+__global__ void __launch_bounds__(256) k_interpolate(DevBuf<T> d, int ni, int nu_out, T *Xo, T *Uo) {
+    const int N = d.N, cx = N * ni, cu = (N - 1) * ni;
+    const long per = 9L * cx + (long)nu_out * cu;
+    const long g = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= (long)d.B * per) return;
+    const int b = (int)(g / per);
+    long e = g % per;
+    if (e < 9L * cx) {
+        const int r = (int)(e / cx), col = (int)(e % cx), i = col / ni, j = col % ni;
+        const T *X = d.Xacc + (size_t)b * (N + 1) * 9;
+        const T v0 = X[(size_t)i * 9 + r], v1 = X[(size_t)(i + 1) * 9 + r];
+        Xo[(size_t)b * 9 * cx + e] = v0 + T(j) * ((v1 - v0) / T(ni));
+    } else {
+        e -= 9L * cx;
+        const int r = (int)(e / cu), col = (int)(e % cu), i = col / ni, j = col % ni;
+        const T *U = d.Uacc + (size_t)b * N * NU;
+        const T v0 = U[(size_t)i * NU + r], v1 = U[(size_t)(i + 1) * NU + r];
+        Uo[(size_t)b * nu_out * cu + e] = v0 + T(j) * ((v1 - v0) / T(ni));
+    }
+}
+template __global__ void k_interpolate<double>(DevBuf<double>, int, int, double *, double *);
+template __global__ void k_interpolate<float>(DevBuf<float>, int, int, float *, float *);
 
 // nonlinear rollout x+_k = x_k + dt F(x_k, u_k) along (X, U) for k = 0..N (reference
 // integrate_dynamics_trajectory, src/centroidal_model.py:243-255; at k = N the reference's JAX

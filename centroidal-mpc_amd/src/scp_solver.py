@@ -151,9 +151,13 @@ def _results(sol, nu, B):
     return out
 
 
-def solve_scp(model, scp_params):
-    """The reference's SCP loop for one model (reference :118-179), run on the device."""
+def solve_scp(model, scp_params, gusto=False):
+    """The reference's SCP loop for one model (reference :118-179), run on the device.
+    ``gusto=True`` moves the linearization point to each accepted solution and iterates until
+    convergence (the GuSTO scheme the reference cites, :113-117; include/cmpc.h
+    CMPC_SCP_MODE_GUSTO); the default reproduces the reference exactly (quirk Q1)."""
     s = model._device_solver(None, scp_params)
+    s.set_scp_mode('gusto' if gusto else 'reference')
     s.solve_scp(fixed_iters=False)
     sol = s.solution()
     log = s.iteration_log()
@@ -166,10 +170,13 @@ def solve_scp(model, scp_params):
     return res
 
 
-def solve_scp_batch(models, scp_params=None, precision='fp64', device=0, fixed_iters=False):
+def solve_scp_batch(models, scp_params=None, precision='fp64', device=0, fixed_iters=False, gusto=False,
+                    n_inner=None):
     """Batched SCP: all ``models`` (one robot and horizon) in one device handle; returns one
     result per model (the reference's dict or False).  ``scp_params`` (optional) overrides every
-    model's conf scp_params."""
+    model's conf scp_params; ``gusto`` selects the GuSTO mode (see solve_scp); with ``n_inner``
+    each result also carries 'interpolated' = interpolate_SCP_solution of its accepted solution
+    with n_inner sub-steps, computed on the device."""
     models = list(models)
     if not models:
         return []
@@ -191,6 +198,13 @@ def solve_scp_batch(models, scp_params=None, precision='fp64', device=0, fixed_i
     batch.validate()
     with Solver(m0._robot, m0._N, batch.B, precision, device) as s:
         s.upload(batch)
+        s.set_scp_mode('gusto' if gusto else 'reference')
         s.solve_scp(fixed_iters=fixed_iters)
         sol = s.solution()
-    return _results(sol, m0._n_u, batch.B)
+        interp = s.interpolate(int(n_inner)) if n_inner else None
+    res = _results(sol, m0._n_u, batch.B)
+    if interp is not None:
+        for b, r in enumerate(res):
+            if r is not False and r['state']:
+                r['interpolated'] = dict(X=interp[0][b], U=interp[1][b][:m0._n_u])
+    return res

@@ -55,6 +55,15 @@ extern "C" {
 #define CMPC_SCP_MAX_ITER 2       /* loop ended on max_iterations / omega_max */
 #define CMPC_SCP_QP_FAILED (-1)   /* reference returns False (src/scp_solver.py:146-148) */
 
+/* SCP modes.  REFERENCE reproduces src/scp_solver.py:118-179 exactly, including quirk Q1: the
+ * linearization point stays at the warm start (traj_tuple is never reassigned, :129-130), so the
+ * loop ends after the first accepted iteration.  GUSTO implements the GuSTO scheme the
+ * reference cites (:113-117): an accepted solution becomes the next linearization point and the
+ * loop runs until convergence(traj, prev) (:51-56, spectral norms) < convergence_threshold.
+ * The tracking cost and the initial / final state constraints stay on the warm start in both. */
+#define CMPC_SCP_MODE_REFERENCE 0
+#define CMPC_SCP_MODE_GUSTO 1
+
 typedef struct cmpc_handle_s *cmpc_handle;
 
 /* Parameters of one problem class: the conf_* attributes the hot path reads
@@ -109,6 +118,9 @@ int cmpc_upload(cmpc_handle h, int B, const int32_t *class_id, const int8_t *log
  * stack_up_all_constraints (reference src/scp_solver.py:28, src/constraints.py:260). */
 int cmpc_set_trust_region(cmpc_handle h, const double *weight, const double *radius);
 
+/* Select the SCP mode for subsequent iterations (default CMPC_SCP_MODE_REFERENCE). */
+int cmpc_set_scp_mode(cmpc_handle h, int mode);
+
 /* Nonlinear rollout of the uploaded problems' dynamics along (X (B,N+1,9), U (B,N,nu)) into
  * out (B,N+1,9); the contact data of the last knot is reused at k = N.  Replaces
  * Centroidal_model.integrate_dynamics_trajectory (reference src/centroidal_model.py:243-255). */
@@ -140,6 +152,14 @@ int cmpc_get_solution(cmpc_handle h, double *X, double *U, double *K, double *Si
                       int32_t *iterations, int32_t *scp_status, double *weight, double *radius);
 int cmpc_get_iteration_log(cmpc_handle h, double *tr_norm, double *rho, int32_t *qp_status,
                            int32_t *qp_iters, int32_t *decision);
+/* Current linearization point (B,N+1,9) / (B,N,nu) and the last convergence measure
+ * ||dU||/||U|| + ||dX||/||X|| of each problem (0 in reference mode, quirk Q1). */
+int cmpc_get_linearization_point(cmpc_handle h, double *X, double *U, double *convergence);
+/* Linear interpolation of the accepted solution with n_inner sub-steps per interval, on the
+ * device: X_out (B,9,N*n_inner), U_out (B,nu,(N-1)*n_inner) in the reference's layout (column
+ * i*n_inner + j = v_i + j (v_{i+1} - v_i) / n_inner).  Replaces interpolate_SCP_solution
+ * (reference src/scp_solver.py:95-111, N_inner = 10). */
+int cmpc_interpolate(cmpc_handle h, int n_inner, double *X_out, double *U_out);
 int cmpc_get_timing(cmpc_handle h, cmpc_timing *t);
 /* Accumulate per-phase HIP-event timings of every cmpc_scp_iterate between begin and end
  * (no host synchronization inside the region; end synchronizes and sums). */

@@ -8,6 +8,14 @@ Restates ``solve_scp`` (src/scp_solver.py:118-179) including its quirks:
 * radius growth is capped at radius0 (Q8).
 ``fixed_iters=True`` keeps iterating to ``max_iterations`` (acceptance still computed), the
 benchmark's fixed-K mode.
+
+``gusto=True`` restates the GuSTO scheme the reference cites (:113-117) but never executes: an
+accepted solution becomes the next linearization point (traj_tuple), the previous one
+prev_traj_dict, and the loop stops after an accepted iteration once
+convergence(traj_tuple, prev_traj_dict) (:51-56, spectral norms) < convergence_threshold.  The
+tracking cost and the initial / final state rows stay on the warm start (sum_up_all_costs and
+the constraint builders read model._init_trajectories).  This is the device's
+CMPC_SCP_MODE_GUSTO.
 """
 import numpy as np
 
@@ -16,7 +24,12 @@ from . import transcription as T
 from .osqp_admm import solve_qp
 
 
-def solve_scp(prob, scp_params, qp=solve_qp, dtype=np.float64, fixed_iters=False, log=None):
+def convergence(Xc, Uc, Xp, Up):
+    """src/scp_solver.py:51-56 on (9, N+1) / (nu, N) arrays."""
+    return (M.spectral_norm(Uc - Up) / M.spectral_norm(Uc) + M.spectral_norm(Xc - Xp) / M.spectral_norm(Xc))
+
+
+def solve_scp(prob, scp_params, qp=solve_qp, dtype=np.float64, fixed_iters=False, log=None, gusto=False):
     """prob: dict(prm=..., N=..., logic, pos, rot, Xbar (9,N+1), Ubar (nu,N)).
 
     Returns the reference's dict(state=[...], control=[...], gains=[...], covs=[...]) or False,
@@ -33,13 +46,15 @@ def solve_scp(prob, scp_params, qp=solve_qp, dtype=np.float64, fixed_iters=False
     weight = float(scp_params['omega0']); radius = float(scp_params['trust_region_radius0'])
     success = False
     it = 0
+    conv = 0.0   # convergence(traj_tuple, prev_traj_dict): identically 0 in the reference (Q1)
     P, q = T.build_cost(N, prm, Xbar)
+    Xl, Ul = Xbar, Ubar   # linearization point (traj_tuple)
     while it < max_iter and weight < omega_max and not (
-            (not fixed_iters) and it != 0 and success and 0.0 < conv_thresh):
+            (not fixed_iters) and it != 0 and success and conv < conv_thresh):
         success = False
-        td = M.compute_trajectory_data(Xbar, Ubar, prob['logic'], prob['pos'], prob['rot'], prm, dtype)
-        A, l, u = T.build_constraints(N, prm, prob['logic'], prob['pos'], prob['rot'], Xbar, Ubar, td,
-                                      weight, radius)
+        td = M.compute_trajectory_data(Xl, Ul, prob['logic'], prob['pos'], prob['rot'], prm, dtype)
+        A, l, u = T.build_constraints(N, prm, prob['logic'], prob['pos'], prob['rot'], Xl, Ul, td,
+                                      weight, radius, Xinit=Xbar)
         res = qp(P, q, A, l, u)
         rec = dict(it=it, weight=weight, radius=radius, status=res.info.status, qp_iter=res.info.iter)
         if res.info.status != 'solved':
@@ -47,10 +62,10 @@ def solve_scp(prob, scp_params, qp=solve_qp, dtype=np.float64, fixed_iters=False
                 rec['decision'] = 'qp_failed'; log.append(rec)
             return False
         X, U = T.get_qp_solution(N, nu, res.x)
-        tr = M.spectral_norm(X - Xbar)
+        tr = M.spectral_norm(X - Xl)
         rec['tr_norm'] = tr
         if tr < radius:
-            rho = float(M.compute_model_accuracy(X, U, Xbar, Ubar, td, prob['logic'], prob['pos'],
+            rho = float(M.compute_model_accuracy(X, U, Xl, Ul, td, prob['logic'], prob['pos'],
                                                  prob['rot'], prm, dtype))
             rec['rho'] = rho
             if rho > rho1:
@@ -63,6 +78,10 @@ def solve_scp(prob, scp_params, qp=solve_qp, dtype=np.float64, fixed_iters=False
                 rec['decision'] = 'accept'
                 if rho < rho0:
                     radius = min(beta_succ * radius, scp_params['trust_region_radius0'])
+                if gusto:
+                    conv = float(convergence(X, U, Xl, Ul))
+                    rec['conv'] = conv
+                    Xl, Ul = X, U
         else:
             weight *= gamma_fail
             rec['decision'] = 'reject_tr'

@@ -80,8 +80,12 @@ class _Rows:
         return sparse.csc_matrix((self.v, (self.r, self.c)), shape=(self.m, self.n))
 
 
-def build_constraints(N, prm, logic, pos, rot, Xbar, Ubar, traj_data, weight, radius):
+def build_constraints(N, prm, logic, pos, rot, Xbar, Ubar, traj_data, weight, radius, Xinit=None):
     """A, l, u of stack_up_all_constraints (src/scp_solver.py:28-48).
+
+    (Xbar, Ubar) is the linearization point (traj_tuple); the initial / final state rows use the
+    warm start ``Xinit`` (model._init_trajectories, src/centroidal_model.py:87-89), which is Xbar
+    itself in the reference's loop (quirk Q1) and the default here.
 
     Row order: init (9) | dynamics (9N) | final (9) | [TALOS CoP: per contact N x-rows then
     N y-rows] | friction (per contact, per knot, 5 rows, rows 0-3 filled when active) |
@@ -90,10 +94,11 @@ def build_constraints(N, prm, logic, pos, rot, Xbar, Ubar, traj_data, weight, ra
     nu = prm['nu']; nc = prm['nc']; nupc = nu // nc
     n = n_vars(N, nu)
     Xbar = np.asarray(Xbar, float); Ubar = np.asarray(Ubar, float)
+    Xi = Xbar if Xinit is None else np.asarray(Xinit, float)
     rows = _Rows(n)
-    # initial constraints (src/constraints.py:11-17): x_init = X_npz[0] = Xbar[:, 0]
+    # initial constraints (src/constraints.py:11-17): x_init = X_npz[0] = Xinit[:, 0]
     for i in range(9):
-        rows.add([i], [1.0], Xbar[i, 0], Xbar[i, 0])
+        rows.add([i], [1.0], Xi[i, 0], Xi[i, 0])
     # dynamics (src/constraints.py:19-50): [A_k  B_k  -I] z = A_k xbar_k + B_k ubar_k - f_k (+-1e-12)
     fdt = traj_data['f_x'].dtype
     for k in range(N):
@@ -108,7 +113,7 @@ def build_constraints(N, prm, logic, pos, rot, Xbar, Ubar, traj_data, weight, ra
             rows.add(cols, vals, lo[i], hi[i])
     # final constraints (src/constraints.py:103-109)
     for i in range(9):
-        rows.add([x_idx(N) + i], [1.0], Xbar[i, N], Xbar[i, N])
+        rows.add([x_idx(N) + i], [1.0], Xi[i, N], Xi[i, N])
     # TALOS CoP (src/constraints.py:111-145)
     if prm['robot'] == 'TALOS':
         lxp, lxn, lyp, lyn = prm['foot_range']

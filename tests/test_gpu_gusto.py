@@ -1,0 +1,82 @@
+"""SURVEY.md 8f row f1 on the GPU: GuSTO mode (the linearization point follows each accepted
+solution) against the oracle's restatement of the same loop, the reference mode's untouched
+linearization point (quirk Q1), and the device interpolate_SCP_solution.
+
+Tolerances: identical iteration counts / accepted counts; accepted X, U and the convergence
+measure within 1e-5 of their scale (the QP solutions are 1e-10-accurate on both sides and
+feed the next linearization); interpolation bit-for-bit up to 1e-14 relative (same formula).
+"""
+import numpy as np
+import pytest
+
+from cmpc._lib import Solver
+from cmpc.synth import make_batch
+from oracle import scp as OS
+from oracle.sparse_ipm import solve_qp as sparse_ipm_qp
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize('cfg,N,B', [('trot', 30, 3), ('bound', 30, 2)])
+def test_gusto_matches_oracle(cfg, N, B):
+    pb = make_batch(cfg, N, B)
+    with Solver(pb.robot, N, B, 'fp64') as s:
+        s.upload(pb)
+        s.set_scp_mode('gusto')
+        s.solve_scp(fixed_iters=False)
+        sol = s.solution()
+        Xl, Ul, conv = s.linearization_point()
+    multi = 0
+    for b in range(B):
+        p = pb.oracle_problem(b)
+        log = []
+        ref = OS.solve_scp(p, p['scp_params'], qp=sparse_ipm_qp, log=log, gusto=True)
+        assert ref is not False
+        assert sol['iterations'][b] == len(log), (sol['iterations'][b], [r['decision'] for r in log])
+        assert sol['n_accepted'][b] == len(ref['state'])
+        multi += len(ref['state']) > 1
+        X, U = ref['state'][-1], ref['control'][-1]
+        np.testing.assert_allclose(sol['X'][b].T, X, rtol=0, atol=1e-5 * np.abs(X).max())
+        np.testing.assert_allclose(sol['U'][b][:, :U.shape[0]].T, U, rtol=0, atol=1e-5 * np.abs(U).max())
+        # the device's linearization point is the last accepted solution
+        np.testing.assert_allclose(Xl[b].T, X, rtol=0, atol=1e-5 * np.abs(X).max())
+        last = [r['conv'] for r in log if 'conv' in r][-1]
+        assert abs(conv[b] - last) <= 1e-5 * max(1.0, abs(last))
+        if sol['status'][b] == 1:
+            assert conv[b] < p['scp_params']['convergence_threshold']
+    assert multi >= 1   # the mode does iterate past the reference's single accepted step
+
+
+def test_reference_mode_keeps_the_warm_start():
+    pb = make_batch('trot', 30, 2)
+    with Solver(pb.robot, 30, 2, 'fp64') as s:
+        s.upload(pb)
+        s.solve_scp(fixed_iters=False)
+        Xl, Ul, conv = s.linearization_point()
+        sol = s.solution()
+    assert np.array_equal(Xl, pb.Xbar) and np.array_equal(Ul[:, :, :pb.Ubar.shape[2]], pb.Ubar)
+    assert np.all(conv == 0.0) and np.all(sol['n_accepted'] <= 1)
+
+
+def test_device_interpolation_matches_reference_formula():
+    N, B, ni = 30, 3, 10
+    pb = make_batch('trot', N, B)
+    with Solver(pb.robot, N, B, 'fp64') as s:
+        s.upload(pb)
+        s.solve_scp(fixed_iters=False)
+        sol = s.solution()
+        Xi, Ui = s.interpolate(ni)
+    for b in range(B):
+        X, U = sol['X'][b].T, sol['U'][b].T
+        # reference src/scp_solver.py:95-111, loop form
+        Xr = np.zeros((9, (X.shape[1] - 1) * ni)); Ur = np.zeros((U.shape[0], (U.shape[1] - 1) * ni))
+        for i in range(U.shape[1] - 1):
+            du = (U[:, i + 1] - U[:, i]) / float(ni)
+            for j in range(ni):
+                Ur[:, i * ni + j] = U[:, i] + j * du
+        for i in range(X.shape[1] - 1):
+            dx = (X[:, i + 1] - X[:, i]) / float(ni)
+            for j in range(ni):
+                Xr[:, i * ni + j] = X[:, i] + j * dx
+        np.testing.assert_allclose(Xi[b], Xr, rtol=1e-14, atol=1e-14)
+        np.testing.assert_allclose(Ui[b], Ur, rtol=1e-14, atol=1e-14)
