@@ -40,6 +40,14 @@ class QPSettings(ctypes.Structure):
                 ('step_fraction', ctypes.c_double)]
 
 
+class Gait(ctypes.Structure):
+    _fields_ = [('type', ctypes.c_int32), ('nb_steps', ctypes.c_int32), ('step_knots', ctypes.c_int32),
+                ('support_knots', ctypes.c_int32), ('step_length', ctypes.c_double)]
+
+
+GAIT_TYPES = {'TROT': 0, 'PACE': 1, 'BOUND': 2}
+
+
 class Timing(ctypes.Structure):
     _fields_ = [('linearize_ms', ctypes.c_float), ('assemble_ms', ctypes.c_float), ('qp_ms', ctypes.c_float),
                 ('accept_ms', ctypes.c_float), ('total_ms', ctypes.c_float)]
@@ -52,7 +60,8 @@ EXPORTS = ['cmpc_create', 'cmpc_destroy', 'cmpc_last_error', 'cmpc_version', 'cm
            'cmpc_get_linearization', 'cmpc_qp_sizes', 'cmpc_export_qp', 'cmpc_get_qp_solution',
            'cmpc_get_solution', 'cmpc_get_iteration_log', 'cmpc_get_timing', 'cmpc_timing_begin',
            'cmpc_timing_end', 'cmpc_get_qp_iterations_total', 'cmpc_debug_stamps', 'cmpc_set_scp_mode',
-           'cmpc_get_linearization_point', 'cmpc_interpolate']
+           'cmpc_get_linearization_point', 'cmpc_interpolate', 'cmpc_generate_contact_plans',
+           'cmpc_upload_states', 'cmpc_get_contact_plans', 'cmpc_get_warm_start']
 SCP_MODE = {'reference': 0, 'gusto': 1}
 
 _lib = None
@@ -103,6 +112,10 @@ def load():
         'cmpc_set_scp_mode': (i32, [h, i32]),
         'cmpc_get_linearization_point': (i32, [h, vp, vp, vp]),
         'cmpc_interpolate': (i32, [h, i32, vp, vp]),
+        'cmpc_generate_contact_plans': (i32, [h, i32, vp, vp]),
+        'cmpc_upload_states': (i32, [h, i32, vp, vp, vp]),
+        'cmpc_get_contact_plans': (i32, [h, vp, vp, vp]),
+        'cmpc_get_warm_start': (i32, [h, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -210,6 +223,41 @@ class Solver:
                       np.ascontiguousarray(pb.Xbar, float), np.ascontiguousarray(pb.Ubar, float)]
         self._chk(self.lib.cmpc_upload(self.h, pb.B, *[_ptr(a) for a in self._keep]), 'cmpc_upload')
         self.B = pb.B
+
+    def generate_contact_plans(self, gaits, foot0):
+        """Contact plans of len(gaits) problems built on the device (cmpc_generate_contact_plans).
+        gaits: conf-style dicts (type, nbSteps, stepKnots, supportKnots, stepLength); foot0 (B, nc, 3)
+        in the contact order FR, FL, HR, HL (solo12) / FR, FL (TALOS)."""
+        B = len(gaits)
+        g = (Gait * B)()
+        for i, gd in enumerate(gaits):
+            g[i].type = GAIT_TYPES[gd['type']]
+            g[i].nb_steps, g[i].step_knots = int(gd['nbSteps']), int(gd['stepKnots'])
+            g[i].support_knots, g[i].step_length = int(gd['supportKnots']), float(gd['stepLength'])
+        f0 = np.ascontiguousarray(foot0, float)
+        if f0.shape != (B, self.nc, 3):
+            raise ValueError('foot0 must be (%d, %d, 3)' % (B, self.nc))
+        self._chk(self.lib.cmpc_generate_contact_plans(self.h, B, g, _ptr(f0)), 'cmpc_generate_contact_plans')
+        self.B = B
+
+    def upload_states(self, params, class_id, Xbar, Ubar=None):
+        """Warm starts for the device-planned problems; Ubar None -> the reference's warm-start
+        controls built on the device."""
+        self.set_params(params)
+        self._keep = [np.ascontiguousarray(class_id, np.int32), np.ascontiguousarray(Xbar, float),
+                      None if Ubar is None else np.ascontiguousarray(Ubar, float)]
+        self._chk(self.lib.cmpc_upload_states(self.h, self.B, *[_ptr(a) for a in self._keep]), 'cmpc_upload_states')
+
+    def contact_plans(self):
+        B, N, nc = self.B, self.N, self.nc
+        lg = np.zeros((B, N, nc), np.int8); pos = np.zeros((B, N, nc, 3)); rot = np.zeros((B, N, nc, 3, 3))
+        self._chk(self.lib.cmpc_get_contact_plans(self.h, _ptr(lg), _ptr(pos), _ptr(rot)), 'cmpc_get_contact_plans')
+        return lg, pos, rot
+
+    def warm_start(self):
+        X = np.zeros((self.B, self.N + 1, 9)); U = np.zeros((self.B, self.N, self.nu))
+        self._chk(self.lib.cmpc_get_warm_start(self.h, _ptr(X), _ptr(U)), 'cmpc_get_warm_start')
+        return X, U
 
     # ---- phases
     def set_trust_region(self, weight=None, radius=None):

@@ -38,8 +38,10 @@ class _PlanConf:
         self.contact_sequence = seq
 
 
-def contact_plan(conf, N, rng=None, jitter=True):
-    """(logic, pos, rot) of N knots for one problem of config ``conf``."""
+def plan_spec(conf, N, rng=None, jitter=True):
+    """(gait, foot0) of one problem: the conf gait dict with the per-problem stepLength and the
+    nbSteps that covers N knots, and the initial foot positions (nc, 3) in the contact order
+    FR, FL, HR, HL / FR, FL (what cmpc_generate_contact_plans takes)."""
     gait = dict(conf.gait)
     robot = copy.deepcopy(conf.rmodel)
     if rng is not None and jitter:
@@ -52,6 +54,19 @@ def contact_plan(conf, N, rng=None, jitter=True):
         if plan_length(seq, conf.dt) >= N:
             break
         gait['nbSteps'] += 1
+    trans = [robot.foot_positions[n] for n in conf.ee_frame_names]
+    feet = {'FL': trans[0], 'FR': trans[1]}
+    order = ('FR', 'FL')
+    if len(trans) == 4:
+        feet['HL'], feet['HR'] = trans[2], trans[3]
+        order = ('FR', 'FL', 'HR', 'HL')
+    foot0 = np.array([feet[c] for c in order], float)
+    return gait, foot0, robot, seq
+
+
+def contact_plan(conf, N, rng=None, jitter=True):
+    """(logic, pos, rot) of N knots for one problem of config ``conf``."""
+    _, _, _, seq = plan_spec(conf, N, rng, jitter)
     traj = create_contact_trajectory(_PlanConf(conf.dt, seq))
     return contact_arrays(traj, N)
 

@@ -19,6 +19,8 @@ template <typename T, int R> __global__ void k_linearize(DevBuf<T>, int);
 template <typename T, int R> __global__ void k_assemble(DevBuf<T>, int);
 template <typename T, int R> __global__ void k_qp_ipm(DevBuf<T>, int, int, T, T, T);
 template <typename T> __global__ void k_interpolate(DevBuf<T>, int, int, T *, T *);
+template <typename T, int R> __global__ void k_contact_plan(DevBuf<T>, const cmpc_gait *, const T *, uint8_t *, T *, T *);
+template <typename T, int R> __global__ void k_default_controls(DevBuf<T>, T *);
 size_t ipm_lds_bytes(int N, int prec_bytes);
 template <typename T, int R> __global__ void k_accept(DevBuf<T>, int);
 template <typename T, int R> __global__ void k_rollout(DevBuf<T>, const T *, const T *, T *);
@@ -99,6 +101,7 @@ struct cmpc_handle_s {
          *Xacc = nullptr, *Uacc = nullptr, *Kacc = nullptr, *Sacc = nullptr, *stamps = nullptr, *Xlin = nullptr,
          *Ulin = nullptr;
     int scp_mode = CMPC_SCP_MODE_REFERENCE;
+    int plans_B = 0;   // problems whose contact plans were built on the device
 
     size_t esz() const { return prec == CMPC_PREC_F64 ? 8 : 4; }
     void *dalloc(size_t bytes) {
@@ -243,6 +246,32 @@ template <typename T> void interpolate_impl(cmpc_handle h, int ni, double *Xo, d
     HIPCHK(hipGetLastError());
     from_dev<T>(h, Xo, dX, nx);
     from_dev<T>(h, Uo, dU, nuo);
+}
+
+template <typename T, int R> void plan_impl(cmpc_handle h, const cmpc_gait *gaits, const double *foot0) {
+    const size_t B = h->B, NC = h->NC;
+    void *dg = nullptr, *df = nullptr;
+    HIPCHK(hipMalloc(&dg, B * sizeof(cmpc_gait)));
+    HIPCHK(hipMalloc(&df, B * NC * 3 * sizeof(T)));
+    struct Free {
+        void *p[2];
+        ~Free() { for (void *q : p) if (q) (void)hipFree(q); }
+    } fr{{dg, df}};
+    HIPCHK(hipMemcpyAsync(dg, gaits, B * sizeof(cmpc_gait), hipMemcpyHostToDevice, h->stream));
+    to_dev<T>(h, df, foot0, B * NC * 3);
+    const long n = (long)B * h->N;
+    hipLaunchKernelGGL((k_contact_plan<T, R>), dim3((unsigned)((n + 127) / 128)), dim3(128), 0, h->stream,
+                       h->buf<T>(), (const cmpc_gait *)dg, (const T *)df, (uint8_t *)h->logic, (T *)h->pos,
+                       (T *)h->rot);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(h->stream));
+}
+
+template <typename T, int R> void default_controls_impl(cmpc_handle h) {
+    const long n = (long)h->B * h->N;
+    hipLaunchKernelGGL((k_default_controls<T, R>), dim3((unsigned)((n + 127) / 128)), dim3(128), 0, h->stream,
+                       h->buf<T>(), (T *)h->Ubar);
+    HIPCHK(hipGetLastError());
 }
 
 template <typename T, int R> void rollout_impl(cmpc_handle h, const double *X, const double *U, double *out) {
@@ -441,6 +470,7 @@ int cmpc_upload(cmpc_handle h, int B, const int32_t *class_id, const int8_t *log
             need(act > 0, "a knot without active contact (the reference divides by zero there)");
         }
         h->B = B;
+        h->plans_B = 0;
         HIPCHK(hipMemcpyAsync(h->class_id, class_id, (size_t)B * 4, hipMemcpyHostToDevice, h->stream));
         HIPCHK(hipMemcpyAsync(h->logic, logic, (size_t)B * N * NC, hipMemcpyHostToDevice, h->stream));
         auto up = [&](void *dst, const double *src, size_t n) {
@@ -467,6 +497,80 @@ int cmpc_set_trust_region(cmpc_handle h, const double *weight, const double *rad
         }
         HIPCHK(hipMemcpyAsync(h->scp, st.data(), st.size() * sizeof(ScpState), hipMemcpyHostToDevice, h->stream));
         HIPCHK(hipStreamSynchronize(h->stream));
+    });
+}
+
+int cmpc_generate_contact_plans(cmpc_handle h, int B, const cmpc_gait *gaits, const double *foot0) {
+    return guard(h, [&] {
+        need(B >= 1 && B <= h->max_batch, "batch size out of range");
+        need(gaits && foot0, "null input buffer");
+        for (int b = 0; b < B; ++b) {
+            const cmpc_gait &g = gaits[b];
+            need(g.type == CMPC_GAIT_TROT || g.type == CMPC_GAIT_PACE || g.type == CMPC_GAIT_BOUND, "unknown gait type");
+            need(g.nb_steps >= 1 && g.step_knots >= 1 && g.support_knots >= 1, "invalid gait knots");
+            need((long)g.nb_steps * 2 * (g.step_knots + g.support_knots) + g.support_knots >= h->N,
+                 "contact plan shorter than the horizon N (raise nb_steps)");
+            need(h->robot == 0 || g.type == CMPC_GAIT_PACE,
+                 "TALOS plans support PACE only (other gaits swing both feet: a knot without active contact)");
+        }
+        h->B = B;
+        if (h->prec == CMPC_PREC_F64) {
+            if (h->robot == 0) plan_impl<double, 0>(h, gaits, foot0); else plan_impl<double, 1>(h, gaits, foot0);
+        } else {
+            if (h->robot == 0) plan_impl<float, 0>(h, gaits, foot0); else plan_impl<float, 1>(h, gaits, foot0);
+        }
+        h->plans_B = B;
+    });
+}
+
+int cmpc_upload_states(cmpc_handle h, int B, const int32_t *class_id, const double *Xbar, const double *Ubar) {
+    return guard(h, [&] {
+        need(h->n_classes > 0, "call cmpc_set_params first");
+        need(h->plans_B == B && B >= 1, "no device contact plans for this batch (cmpc_generate_contact_plans)");
+        need(class_id && Xbar, "null input buffer");
+        for (int b = 0; b < B; ++b) need(class_id[b] >= 0 && class_id[b] < h->n_classes, "class_id out of range");
+        const int N = h->N;
+        h->B = B;
+        HIPCHK(hipMemcpyAsync(h->class_id, class_id, (size_t)B * 4, hipMemcpyHostToDevice, h->stream));
+        auto up = [&](void *dst, const double *src, size_t n) {
+            if (h->prec == CMPC_PREC_F64) to_dev<double>(h, dst, src, n); else to_dev<float>(h, dst, src, n);
+        };
+        up(h->Xbar, Xbar, (size_t)B * (N + 1) * 9);
+        if (Ubar) {
+            up(h->Ubar, Ubar, (size_t)B * N * NU);
+        } else if (h->prec == CMPC_PREC_F64) {
+            if (h->robot == 0) default_controls_impl<double, 0>(h); else default_controls_impl<double, 1>(h);
+        } else {
+            if (h->robot == 0) default_controls_impl<float, 0>(h); else default_controls_impl<float, 1>(h);
+        }
+        HIPCHK(hipMemcpyAsync(h->Xlin, h->Xbar, (size_t)B * (N + 1) * 9 * h->esz(), hipMemcpyDeviceToDevice, h->stream));
+        HIPCHK(hipMemcpyAsync(h->Ulin, h->Ubar, (size_t)B * N * NU * h->esz(), hipMemcpyDeviceToDevice, h->stream));
+        reset_scp(h, class_id);
+    });
+}
+
+int cmpc_get_contact_plans(cmpc_handle h, int8_t *logic, double *pos, double *rot) {
+    return guard(h, [&] {
+        need(h->B > 0, "no problems uploaded");
+        const size_t B = h->B, N = h->N, NC = h->NC;
+        auto dl = [&](double *dst, void *src, size_t n) {
+            if (h->prec == CMPC_PREC_F64) from_dev<double>(h, dst, src, n); else from_dev<float>(h, dst, src, n);
+        };
+        if (logic) from_dev_raw(h, logic, h->logic, B * N * NC);
+        dl(pos, h->pos, B * N * NC * 3);
+        dl(rot, h->rot, B * N * NC * 9);
+    });
+}
+
+int cmpc_get_warm_start(cmpc_handle h, double *Xbar, double *Ubar) {
+    return guard(h, [&] {
+        need(h->B > 0, "no problems uploaded");
+        const size_t B = h->B, N = h->N;
+        auto dl = [&](double *dst, void *src, size_t n) {
+            if (h->prec == CMPC_PREC_F64) from_dev<double>(h, dst, src, n); else from_dev<float>(h, dst, src, n);
+        };
+        dl(Xbar, h->Xbar, B * (N + 1) * 9);
+        dl(Ubar, h->Ubar, B * N * NU);
     });
 }
 

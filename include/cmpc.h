@@ -118,6 +118,33 @@ int cmpc_upload(cmpc_handle h, int B, const int32_t *class_id, const int8_t *log
  * stack_up_all_constraints (reference src/scp_solver.py:28, src/constraints.py:260). */
 int cmpc_set_trust_region(cmpc_handle h, const double *weight, const double *radius);
 
+/* ---- on-device contact plans (replaces the host construction of src/contact_plan.py:40-48,
+ * 112-264 and src/centroidal_model.py:127-187 for large batches) ---- */
+#define CMPC_GAIT_TROT 0
+#define CMPC_GAIT_PACE 1
+#define CMPC_GAIT_BOUND 2
+typedef struct {
+    int32_t type;            /* CMPC_GAIT_* (conf gait['type']) */
+    int32_t nb_steps;        /* gait['nbSteps'] */
+    int32_t step_knots;      /* gait['stepKnots'] */
+    int32_t support_knots;   /* gait['supportKnots'] */
+    double step_length;      /* gait['stepLength'] */
+} cmpc_gait;
+/* Build the contact plans of B problems on the device: phases [support, step A, support, step B]
+ * x nb_steps + support, swing feet inactive, stance feet at foot0 advanced by step_length per
+ * completed step (bit-identical to the host construction), identity rotations.
+ * foot0 (B, nc, 3) in the contact order FR, FL, HR, HL (solo12) / FR, FL (TALOS).  The plan must
+ * cover N knots; every knot needs an active contact (TALOS supports only PACE). */
+int cmpc_generate_contact_plans(cmpc_handle h, int B, const cmpc_gait *gaits, const double *foot0);
+/* Upload warm starts for the B problems whose plans are on the device and reset their SCP state
+ * (as cmpc_upload).  Ubar == NULL fills the reference's warm-start controls on the device
+ * (src/centroidal_model.py:176-183). */
+int cmpc_upload_states(cmpc_handle h, int B, const int32_t *class_id, const double *Xbar, const double *Ubar);
+/* Read the device contact plans back: logic (B,N,nc) int8, pos (B,N,nc,3), rot (B,N,nc,9). */
+int cmpc_get_contact_plans(cmpc_handle h, int8_t *logic, double *pos, double *rot);
+/* Read the warm-start controls (B,N,nu) (e.g. after cmpc_upload_states with Ubar == NULL). */
+int cmpc_get_warm_start(cmpc_handle h, double *Xbar, double *Ubar);
+
 /* Select the SCP mode for subsequent iterations (default CMPC_SCP_MODE_REFERENCE). */
 int cmpc_set_scp_mode(cmpc_handle h, int mode);
 
