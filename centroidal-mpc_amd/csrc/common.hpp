@@ -13,7 +13,7 @@ namespace cmpc {
 
 constexpr int NX = 9;
 constexpr int NU = 12;
-constexpr int IPM_NT = 128;   // threads per QP workgroup (one problem)
+constexpr int IPM_NT = 64;    // threads per QP workgroup (one problem, one wave)
 constexpr int WAVE = 64;
 
 template <int ROBOT> struct Robot;

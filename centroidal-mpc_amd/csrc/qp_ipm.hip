@@ -34,7 +34,7 @@
 
 namespace cmpc {
 
-constexpr int NT = IPM_NT;   // two waves: the two ends of the Schur sweeps; knots k, k + 128, ...
+constexpr int NT = IPM_NT;   // one wave: a half-wave per end of the Schur sweeps; knots k, k + 64, ...
 constexpr int FU = 34;   // per-contact factor record: Gw 12 | Kinv 10 | F 6 | Winvd 6
 // per-knot (x, t) factor record: 1/Wx[0:6] | M_LL packed 6 | chol(K_TR) packed 36 (diagonal as 1/L_jj) | z1 = L^-1 1 (8) |
 // 1/den | D_slack  (K_TR = D_TR^-1 + G_L W_L^-1 G_L', see phase_factor)
@@ -702,18 +702,18 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_sblock(const C
 }
 
 // (4) two-ended ("twisted") block-Thomas factorization of the SPD block-tridiagonal S with
-// explicit symmetric inverses.  Wave 0 eliminates from the top, wave 1 from the bottom, and the
-// two meet at block m:
+// explicit symmetric inverses.  Lanes 0..31 eliminate from the top, lanes 32..63 from the bottom
+// (one wave per problem, so four problems share a CU), and the two ends meet at block m:
 //   top    (j < m):  X_j = S_{j,j-1} I_{j-1},  I_j = (S_jj - X_j S_{j-1,j})^-1      So[j-1] <- X_j
 //   bottom (j > m):  Y_j = S_{j,j+1} I_{j+1},  I_j = (S_jj - Y_j S_{j+1,j})^-1      So[j]   <- Y_j
 //   meet   (j = m):  I_m = (S_mm - X_m S_{m-1,m} - Y_m S_{m+1,m})^-1
 // Sd[j] holds S_jj on input and I_j on output, So[j] holds S_{j,j+1} on input (both in the
-// workspace, so the kernel's LDS stays small and several problems share a CU).  Each wave keeps
-// its previous inverse and the step's blocks in a small LDS scratch; the next step's raw blocks
-// are fetched one step ahead (a step is thousands of cycles).  Inverses by Gauss-Jordan sweeps
-// over the 64 lanes (SPD: no pivoting) with a pivot floor relative to the original diagonal
-// (near the solution of a degenerate QP the Schur blocks are differences of O(M) numbers).
-// Per-wave LDS scratch: A (current) | P (previous inverse) | Xb | Ob | Dd (original diagonal) | Dn (S_jj).
+// workspace, so the kernel's LDS stays small and several problems share a CU).  Each half-wave
+// keeps its previous inverse and the step's blocks in a small LDS scratch; the next step's raw
+// blocks are fetched one step ahead (a step is thousands of cycles).  Inverses by Gauss-Jordan
+// sweeps over the 32 lanes of a half (SPD: no pivoting) with a pivot floor relative to the
+// original diagonal (near the solution of a degenerate QP the Schur blocks are differences of
+// O(M) numbers).  Per-half LDS scratch: A (current) | P (previous inverse) | Xb | Ob | Dd (original diagonal) | Dn (S_jj).
 template <typename T> __device__ __forceinline__ T dot9(const LdsT<T> *a, const LdsT<T> *b) {
     T av[9], bv[9];
 #pragma unroll
@@ -725,33 +725,46 @@ template <typename T> __device__ __forceinline__ T dot9(const LdsT<T> *a, const 
 }
 constexpr int TW_SCRATCH = 5 * 88 + 16;
 
+// One step over L lanes: L = 32 is a half-wave (one end of the twisted recurrence), L = 64 the
+// whole wave (the meeting block).  Lane l of the group holds the NE = ceil(81 / L) elements
+// e = l + L q of the 9x9 blocks (the last one clamped and masked past 80).
 // With vb != nullptr the step also runs the forward elimination of the right-hand side held in
-// vb (the predictor's, known before the factorization): y_j = b_j - X_j y_jx (top), or
-// b_j - Y_j y_jy (bottom), or at the meeting block x_m = I_m (b_m - X_m y_{m-1} - Y_m y_{m+1}),
-// with X_j / Y_j read from the LDS scratch while they are there.
-template <typename T>
+// vb (the predictor's, known before the factorization): y_j = b_j - X_j y_jx (an end), or at the
+// meeting block x_m = I_m (b_m - X_m y_{m-1} - Y_m y_{m+1}), with X_j / Y_j read from the LDS
+// scratch while they are there.
+//   Op, Ip: X = Op' Ip, A -= X Op   (Op = S_{j-1,j}; the bottom end lands S_{j,j+1}' here, so
+//           the same code forms Y_j = S_{j,j+1} I_{j+1} and A -= Y_j S_{j,j+1}')
+//   Oq, Iq: Y = Oq Iq, A -= Y Oq'   (meeting block only)
+template <typename T, int L>
 __device__ __forceinline__ void tw_step(const LdsT<T> *Dn, const LdsT<T> *Op, const LdsT<T> *Ip, const LdsT<T> *Oq,
                                         const LdsT<T> *Iq, T *Xout, T *Yout, T *Iout, LdsT<T> *A, LdsT<T> *P,
                                         LdsT<T> *Xb, LdsT<T> *Dd, LdsT<T> *vb = nullptr, int j = 0, int jx = 0,
                                         int jy = 0, unsigned long long *sub = nullptr) {
+    constexpr int NE = (81 + L - 1) / L;
 #ifdef CMPC_STAMPS
     unsigned long long tq = __builtin_amdgcn_s_memtime();
 #define SUBSTAMP(i) do { if (sub) { const unsigned long long tn = __builtin_amdgcn_s_memtime(); sub[i] += tn - tq; tq = tn; } } while (0)
 #else
 #define SUBSTAMP(i) do { } while (0)
 #endif
-    const int lane = threadIdx.x & 63;
-    const int e0 = lane, e1 = lane + 64;
-    const bool has1 = e1 < 81;
-    const int i0 = e0 / 9, c0 = e0 % 9, i1 = e1 / 9, c1 = e1 % 9;
-    const T d0 = Dn[e0], d1 = has1 ? Dn[e1] : T(0);
-    T a0 = d0, a1 = d1;
-    T rv = (vb && lane < 9) ? vb[j * 9 + lane] : T(0);   // b_j (fused elimination)
-    // original diagonal of S_jj (pivot floor): entries 0, 10, ..., 60 are lanes' first elements,
-    // 70 and 80 second elements
-    if (e0 % 10 == 0) Dd[e0 / 10] = d0;
-    if (has1 && e1 % 10 == 0) Dd[e1 / 10] = d1;
-    T x0 = T(0), x1 = T(0), y0 = T(0), y1 = T(0);
+    const int l = threadIdx.x & (L - 1);
+    int e[NE], ii[NE], cc[NE];
+    bool ok[NE];
+#pragma unroll
+    for (int q = 0; q < NE; ++q) {
+        ok[q] = l + L * q < 81;
+        e[q] = ok[q] ? l + L * q : 80;
+        ii[q] = e[q] / 9;
+        cc[q] = e[q] % 9;
+    }
+    T a[NE], x[NE], y[NE];
+#pragma unroll
+    for (int q = 0; q < NE; ++q) { a[q] = Dn[e[q]]; x[q] = T(0); y[q] = T(0); }
+    T rv = (vb && l < 9) ? vb[j * 9 + l] : T(0);   // b_j (fused elimination)
+    // original diagonal of S_jj (pivot floor): entries 0, 10, ..., 80
+#pragma unroll
+    for (int q = 0; q < NE; ++q)
+        if (ok[q] && e[q] % 10 == 0) Dd[e[q] / 10] = a[q];
     // 9-term dot products with every LDS operand read before the first multiply
     auto dot = [&](auto fa, auto fb) -> T {
         T u[9], v[9];
@@ -762,32 +775,41 @@ __device__ __forceinline__ void tw_step(const LdsT<T> *Dn, const LdsT<T> *Op, co
         for (int m = 3; m < 9; m += 3) { s0 = fma(u[m], v[m], s0); s1 = fma(u[m + 1], v[m + 1], s1); s2 = fma(u[m + 2], v[m + 2], s2); }
         return s0 + s1 + s2;
     };
-    if (Op) {   // X = Op' I_{j-1};  A -= X Op   (Op = S_{j-1,j})
-        x0 = dot([&](int m) { return Op[m * 9 + i0]; }, [&](int m) { return Ip[m * 9 + c0]; });
-        if (has1) x1 = dot([&](int m) { return Op[m * 9 + i1]; }, [&](int m) { return Ip[m * 9 + c1]; });
-        Xb[e0] = x0;
-        if (has1) Xb[e1] = x1;
+    if (Op) {   // X = Op' I_{j-1};  A -= X Op
+#pragma unroll
+        for (int q = 0; q < NE; ++q)
+            x[q] = dot([&](int m) { return Op[m * 9 + ii[q]]; }, [&](int m) { return Ip[m * 9 + cc[q]]; });
+#pragma unroll
+        for (int q = 0; q < NE; ++q)
+            if (ok[q]) Xb[e[q]] = x[q];
         wave_sync();
-        if (vb && lane < 9) rv -= dot9(Xb + lane * 9, vb + jx * 9);
-        a0 -= dot([&](int m) { return Xb[i0 * 9 + m]; }, [&](int m) { return Op[m * 9 + c0]; });
-        if (has1) a1 -= dot([&](int m) { return Xb[i1 * 9 + m]; }, [&](int m) { return Op[m * 9 + c1]; });
+        if (vb && l < 9) rv -= dot9(Xb + l * 9, vb + jx * 9);
+#pragma unroll
+        for (int q = 0; q < NE; ++q)
+            a[q] -= dot([&](int m) { return Xb[ii[q] * 9 + m]; }, [&](int m) { return Op[m * 9 + cc[q]]; });
         wave_sync();
     }
     if (Oq) {   // Y = Oq I_{j+1};  A -= Y Oq'   (Oq = S_{j,j+1})
-        y0 = dot([&](int m) { return Oq[i0 * 9 + m]; }, [&](int m) { return Iq[m * 9 + c0]; });
-        if (has1) y1 = dot([&](int m) { return Oq[i1 * 9 + m]; }, [&](int m) { return Iq[m * 9 + c1]; });
-        Xb[e0] = y0;
-        if (has1) Xb[e1] = y1;
+#pragma unroll
+        for (int q = 0; q < NE; ++q)
+            y[q] = dot([&](int m) { return Oq[ii[q] * 9 + m]; }, [&](int m) { return Iq[m * 9 + cc[q]]; });
+#pragma unroll
+        for (int q = 0; q < NE; ++q)
+            if (ok[q]) Xb[e[q]] = y[q];
         wave_sync();
-        if (vb && lane < 9) rv -= dot9(Xb + lane * 9, vb + jy * 9);
-        a0 -= dot([&](int m) { return Xb[i0 * 9 + m]; }, [&](int m) { return Oq[c0 * 9 + m]; });
-        if (has1) a1 -= dot([&](int m) { return Xb[i1 * 9 + m]; }, [&](int m) { return Oq[c1 * 9 + m]; });
+        if (vb && l < 9) rv -= dot9(Xb + l * 9, vb + jy * 9);
+#pragma unroll
+        for (int q = 0; q < NE; ++q)
+            a[q] -= dot([&](int m) { return Xb[ii[q] * 9 + m]; }, [&](int m) { return Oq[cc[q] * 9 + m]; });
         wave_sync();
     }
-    A[e0] = a0;
-    if (has1) A[e1] = a1;
-    if (Op) { Xout[e0] = x0; if (has1) Xout[e1] = x1; }
-    if (Oq) { Yout[e0] = y0; if (has1) Yout[e1] = y1; }
+#pragma unroll
+    for (int q = 0; q < NE; ++q) {
+        if (!ok[q]) continue;
+        A[e[q]] = a[q];
+        if (Op) Xout[e[q]] = x[q];
+        if (Oq) Yout[e[q]] = y[q];
+    }
     wave_sync();
     SUBSTAMP(0);
     // Gauss-Jordan, branch-free, with the next pivot's reciprocal computed one pivot ahead: every
@@ -796,39 +818,41 @@ __device__ __forceinline__ void tw_step(const LdsT<T> *Dn, const LdsT<T> *Op, co
     T ip = rcp_nr(fmax(A[0], T(1e-13) * Dd[0]));
 #pragma unroll
     for (int c = 0; c < 9; ++c) {
-        const T aic0 = A[i0 * 9 + c], acj0 = A[c * 9 + c0];
-        const T aic1 = A[(has1 ? i1 : 0) * 9 + c], acj1 = A[c * 9 + (has1 ? c1 : 0)];
+        T aic[NE], acj[NE];
+#pragma unroll
+        for (int q = 0; q < NE; ++q) { aic[q] = A[ii[q] * 9 + c]; acj[q] = A[c * 9 + cc[q]]; }
         T ipn = T(0);
         if (c < 8) {
             const T ncc = A[(c + 1) * 9 + c + 1], nic = A[(c + 1) * 9 + c], nci = A[c * 9 + c + 1];
             ipn = rcp_nr(fmax(fma(-(nic * ip), nci, ncc), T(1e-13) * Dd[c + 1]));
         }
-        auto upd = [&](int i, int cc, T aic, T acj, T aij) -> T {
-            const T mi = aic * ip;
-            const T gen = fma(-mi, acj, aij), row = acj * ip, col = -mi;
-            return i == c ? (cc == c ? ip : row) : (cc == c ? col : gen);
-        };
-        a0 = upd(i0, c0, aic0, acj0, a0);
-        a1 = upd(i1, c1, aic1, acj1, a1);
+#pragma unroll
+        for (int q = 0; q < NE; ++q) {
+            const T mi = aic[q] * ip;
+            const T gen = fma(-mi, acj[q], a[q]), row = acj[q] * ip, col = -mi;
+            a[q] = ii[q] == c ? (cc[q] == c ? ip : row) : (cc[q] == c ? col : gen);
+        }
         wave_sync();
-        A[e0] = a0;
-        if (has1) A[e1] = a1;
+#pragma unroll
+        for (int q = 0; q < NE; ++q)
+            if (ok[q]) A[e[q]] = a[q];
         wave_sync();
         ip = ipn;
     }
     SUBSTAMP(1);
-    const T r0 = A[e0], r1 = has1 ? A[e1] : T(0);
-    P[e0] = r0;
-    if (has1) P[e1] = r1;
-    Iout[e0] = r0;
-    if (has1) Iout[e1] = r1;
+#pragma unroll
+    for (int q = 0; q < NE; ++q) {
+        if (!ok[q]) continue;
+        P[e[q]] = a[q];
+        Iout[e[q]] = a[q];
+    }
     if (vb) {
         if (Op && Oq) {   // meeting block: x_m = I_m (b_m - X_m y_{m-1} - Y_m y_{m+1})
-            if (lane < 9) Xb[lane] = rv;
+            if (l < 9) Xb[l] = rv;
             wave_sync();
-            if (lane < 9) vb[j * 9 + lane] = dot9(A + lane * 9, Xb);
-        } else if (lane < 9) {
-            vb[j * 9 + lane] = rv;
+            if (l < 9) vb[j * 9 + l] = dot9(A + l * 9, Xb);
+        } else if (l < 9) {
+            vb[j * 9 + l] = rv;
         }
     }
     wave_sync();
@@ -836,57 +860,72 @@ __device__ __forceinline__ void tw_step(const LdsT<T> *Dn, const LdsT<T> *Op, co
 #undef SUBSTAMP
 }
 
-// the two ends (threads 0..127: wave 0 top blocks 0..m-1, wave 1 bottom blocks NB-1..m+1).  The
-// raw blocks of step s + 1 are loaded during step s and landed in LDS at its end, inside the same
-// loop iteration: registers carried over the back-edge with loads in flight would make the
-// compiler drain the whole memory queue (this step's stores included) at the loop header.
+// the two ends, one per half-wave: lanes 0..31 the top blocks 0..m-1, lanes 32..63 the bottom
+// blocks NB-1..m+1 (for even NB the top end has one step more; the bottom half idles in it).
+// The raw blocks of step s + 1 are loaded during step s and landed in LDS at its end, inside
+// the same loop iteration: registers carried over the back-edge with loads in flight would make
+// the compiler drain the whole memory queue (this step's stores included) at the loop header.
+// The bottom end lands its coupling block S_{j,j+1} transposed, so both ends run the same step.
 template <typename T>
 __device__ void tw_factor_ends(T *Sd, T *So, int NB, int m, LdsT<T> *sh, LdsT<T> *vb, unsigned long long *stamp_out) {
-    const int lane = threadIdx.x & 63;
-    const int e0 = lane, e1 = lane + 64;
-    const bool has1 = e1 < 81;
-    const bool top = (threadIdx.x >> 6) == 0;
+    constexpr int NE = 3;
+    const int lane = threadIdx.x & 63, l = lane & 31;
+    const bool top = lane < 32;
     LdsT<T> *A = sh + (top ? 0 : TW_SCRATCH), *P = A + 88, *Xb = A + 176, *Ob = A + 264, *Dd = A + 352,
             *Dn = A + 368;
     const int j0 = top ? 0 : NB - 1, dj = top ? 1 : -1, nstep = top ? m : NB - 1 - m;
-    auto land = [&](LdsT<T> *dst, T v0, T v1) { dst[e0] = v0; if (has1) dst[e1] = v1; };
+    int e[NE], et[NE];
+    bool ok[NE];
+#pragma unroll
+    for (int q = 0; q < NE; ++q) {
+        ok[q] = l + 32 * q < 81;
+        e[q] = ok[q] ? l + 32 * q : 80;
+        et[q] = top ? e[q] : (e[q] % 9) * 9 + e[q] / 9;   // landing slot of a coupling element
+    }
     unsigned long long sub[4] = {0, 0, 0, 0};
-    unsigned long long *subp = stamp_out ? sub : nullptr;
+    unsigned long long *subp = (stamp_out && top) ? sub : nullptr;
     {
         const T *D0 = Sd + (size_t)j0 * 81;
-        land(Dn, D0[e0], D0[has1 ? e1 : 80]);
+        T v[NE];
+#pragma unroll
+        for (int q = 0; q < NE; ++q) v[q] = D0[e[q]];
+#pragma unroll
+        for (int q = 0; q < NE; ++q)
+            if (ok[q]) Dn[e[q]] = v[q];
     }
     wave_sync();
-    for (int s = 0, j = j0; s < nstep; ++s, j += dj) {
+    for (int s = 0, j = j0; s < m; ++s, j += dj) {
+        const bool act = s < nstep;
         // raw blocks of the next step (clamped past the end: branch-free loads)
         const int jn = s + 1 < nstep ? j + dj : j;
-        const T *On = So + (size_t)(top ? jn - 1 : jn) * 81, *Dnx = Sd + (size_t)jn * 81;
-        const T p0 = On[e0], p1 = On[has1 ? e1 : 80], n0 = Dnx[e0], n1 = Dnx[has1 ? e1 : 80];
-        if (s == 0)
-            tw_step<T>(Dn, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, Sd + (size_t)j * 81, A, P, Xb, Dd,
-                       vb, j, 0, 0, subp);
-        else if (top)
-            tw_step<T>(Dn, Ob, P, nullptr, nullptr, So + (size_t)(j - 1) * 81, nullptr, Sd + (size_t)j * 81, A, P,
-                       Xb, Dd, vb, j, j - 1, 0, subp);
-        else
-            tw_step<T>(Dn, nullptr, nullptr, Ob, P, nullptr, So + (size_t)j * 81, Sd + (size_t)j * 81, A, P, Xb,
-                       Dd, vb, j, 0, j + 1, subp);
+        const T *On = So + (size_t)(top ? (jn > 0 ? jn - 1 : 0) : jn) * 81, *Dnx = Sd + (size_t)jn * 81;
+        T pv[NE], nv[NE];
+#pragma unroll
+        for (int q = 0; q < NE; ++q) { pv[q] = On[e[q]]; nv[q] = Dnx[e[q]]; }
+        if (act) {
+            if (s == 0)
+                tw_step<T, 32>(Dn, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, Sd + (size_t)j * 81, A, P,
+                               Xb, Dd, vb, j, 0, 0, subp);
+            else
+                tw_step<T, 32>(Dn, Ob, P, nullptr, nullptr, So + (size_t)(top ? j - 1 : j) * 81, nullptr,
+                               Sd + (size_t)j * 81, A, P, Xb, Dd, vb, j, j - dj, 0, subp);
+        }
 #ifdef CMPC_STAMPS
         const unsigned long long tl = __builtin_amdgcn_s_memtime();
 #endif
-        land(Ob, p0, p1);
-        land(Dn, n0, n1);
+#pragma unroll
+        for (int q = 0; q < NE; ++q)
+            if (ok[q]) { Ob[et[q]] = pv[q]; Dn[e[q]] = nv[q]; }
         wave_sync();
 #ifdef CMPC_STAMPS
-        sub[3] += __builtin_amdgcn_s_memtime() - tl;
+        if (subp) sub[3] += __builtin_amdgcn_s_memtime() - tl;
 #endif
     }
-    if (stamp_out && lane == 0 && top)
+    if (stamp_out && lane == 0)
         for (int i = 0; i < 4; ++i) stamp_out[12 + i] += sub[i];
 }
 
-// the meeting block (wave 0, after a workgroup barrier): I_{m-1} and I_{m+1} are the two waves'
-// previous inverses in LDS
+// the meeting block (whole wave): I_{m-1} and I_{m+1} are the two halves' previous inverses in LDS
 template <typename T> __device__ void tw_factor_meet(T *Sd, T *So, int m, LdsT<T> *sh, LdsT<T> *vb) {
     const int lane = threadIdx.x & 63;
     const int e0 = lane, e1 = lane + 64;
@@ -900,84 +939,86 @@ template <typename T> __device__ void tw_factor_meet(T *Sd, T *So, int m, LdsT<T
     Dn[e0] = Sd[(size_t)m * 81 + e0];
     if (has1) Dn[e1] = Sd[(size_t)m * 81 + e1];
     wave_sync();
-    tw_step<T>(Dn, Op, P, Oq, Pq, So + (size_t)(m - 1) * 81, So + (size_t)m * 81, Sd + (size_t)m * 81, A, P,
-               Xb, Dd, vb, m, m - 1, m + 1);
+    tw_step<T, 64>(Dn, Op, P, Oq, Pq, So + (size_t)(m - 1) * 81, So + (size_t)m * 81, Sd + (size_t)m * 81, A, P,
+                   Xb, Dd, vb, m, m - 1, m + 1);
 }
 
-// Chunked, double-buffered stream of 9x9 blocks from the workspace into per-wave LDS: each sweep
-// iteration issues the next K blocks (two elements per lane, coalesced), runs K sweep steps out of
-// the current LDS chunk, then lands the next chunk, so one chunk's L2 / Infinity-Cache latency
-// hides behind K dependent steps.  Loads, their landing and their use stay inside one loop
-// iteration (no in-flight registers carried over the back-edge, where the compiler's wait
-// counting would drain the queue), and the loads are branch-free (a clamped index past the end
-// re-reads the last block).
+// Chunked, double-buffered stream of 9x9 blocks from the workspace into a half-wave's LDS ring:
+// each sweep iteration issues the next K blocks (three elements per lane, coalesced), runs K
+// sweep steps out of the current LDS chunk, then lands the next chunk, so one chunk's L2 /
+// Infinity-Cache latency hides behind K dependent steps.  Loads, their landing and their use
+// stay inside one loop iteration (no in-flight registers carried over the back-edge, where the
+// compiler's wait counting would drain the queue), and the loads are branch-free (a clamped
+// index past the end re-reads the last block).
 constexpr int RSLOT = 88;
 template <typename T, int K> struct ChunkStream {
     const T *base;   // block i at base + i * step
     long step;
     int n;
     LdsT<T> *buf;    // 2 x K slots of RSLOT
-    T r0[K], r1[K];
+    T r[K][3];
     __device__ __forceinline__ void issue(int c) {
-        const int lane = threadIdx.x & 63;
+        const int l = threadIdx.x & 31;
 #pragma unroll
         for (int q = 0; q < K; ++q) {
             const int i = c * K + q;
             const T *p = base + (i < n ? i : n - 1) * step;
-            r0[q] = p[lane];
-            r1[q] = p[lane + 64 < 81 ? lane + 64 : 80];
+#pragma unroll
+            for (int g = 0; g < 3; ++g) r[q][g] = p[l + 32 * g < 81 ? l + 32 * g : 80];
         }
     }
     __device__ __forceinline__ void land(int c) {
-        const int lane = threadIdx.x & 63;
+        const int l = threadIdx.x & 31;
         LdsT<T> *b = buf + (c & 1) * K * RSLOT;
 #pragma unroll
-        for (int q = 0; q < K; ++q) {
-            b[q * RSLOT + lane] = r0[q];
-            if (lane + 64 < 81) b[q * RSLOT + lane + 64] = r1[q];
-        }
+        for (int q = 0; q < K; ++q)
+#pragma unroll
+            for (int g = 0; g < 3; ++g)
+                if (l + 32 * g < 81) b[q * RSLOT + l + 32 * g] = r[q][g];
     }
     __device__ __forceinline__ const LdsT<T> *blk(int i) const {
         return buf + ((i / K) & 1) * K * RSLOT + (i % K) * RSLOT;
     }
 };
 constexpr int KE = 8, KB = 4;   // chunk sizes of the elimination (one stream) and back (two) sweeps
-constexpr int SWEEP_LDS = 2 * KE * RSLOT;   // per wave: 2 x 8 slots = 2 x (2 x 4) slots
+constexpr int SWEEP_LDS = 2 * KE * RSLOT;   // per half-wave: 2 x 8 slots = 2 x (2 x 4) slots
 
-// (5c) two-ended block sweeps with the twisted factors: rhs -> dnu in place in the LDS vector vb
+// (5c) two-ended block sweeps with the twisted factors (one end per half-wave): rhs -> dnu in
+// place in the LDS vector vb
 //   top:    y_0 = b_0, y_j = b_j - X_j y_{j-1}           bottom: y_j = b_j - Y_j y_{j+1}
 //   meet:   x_m = I_m (b_m - X_m y_{m-1} - Y_m y_{m+1})
 //   up:     x_j = I_j y_j - X_{j+1}' x_{j+1}  (j < m)   down: x_j = I_j y_j - Y_{j-1}' x_{j-1}  (j > m)
-// X_j sits at So[j-1], Y_j at So[j].  Three stages separated by workgroup barriers.
+// X_j sits at So[j-1], Y_j at So[j].  Three stages separated by workgroup barriers; each half
+// uses 9 of its lanes per step and its own block ring.
 template <typename T> __device__ void tw_solve_elim(const T *Xs, int NB, int m, LdsT<T> *vb, LdsT<T> *ring) {
-    const int lane = threadIdx.x & 63;
-    const bool top = (threadIdx.x >> 6) == 0;
-    const int lr = lane < 9 ? lane : 0;
+    const int lane = threadIdx.x & 63, l = lane & 31;
+    const bool top = lane < 32;
+    const int lr = l < 9 ? l : 0;
     // step i: top j = i + 1 (X_j at So[i]); bottom j = NB - 2 - i (Y_j at So[NB - 2 - i])
-    const int n = top ? m - 1 : NB - 2 - m;
-    ChunkStream<T, KE> X{top ? Xs : Xs + (size_t)(NB - 2) * 81, top ? 81L : -81L, n, ring, {}, {}};
+    const int n = top ? m - 1 : NB - 2 - m, nmax = m - 1;
+    ChunkStream<T, KE> X{top ? Xs : Xs + (size_t)(NB - 2) * 81, top ? 81L : -81L, n > 0 ? n : 1, ring, {}};
     X.issue(0);
     X.land(0);
-    for (int c = 0; c * KE < n; ++c) {
+    for (int c = 0; c * KE < nmax; ++c) {
         X.issue(c + 1);
         wave_sync();
         for (int q = 0; q < KE; ++q) {
             const int i = c * KE + q;
-            if (i >= n) break;
+            if (i >= nmax) break;
             const int j = top ? i + 1 : NB - 2 - i, jp = top ? j - 1 : j + 1;
-            if (lane < 9) {
+            if (l < 9 && i < n) {
                 const LdsT<T> *xr = X.blk(i) + lr * 9;
                 const LdsT<T> *yp = vb + jp * 9;
                 T xv[9], yv[9];
 #pragma unroll
                 for (int e = 0; e < 9; ++e) { xv[e] = xr[e]; yv[e] = yp[e]; }
-                const T bj = vb[j * 9 + lane];
+                const T bj = vb[j * 9 + l];
                 T s0 = xv[0] * yv[0], s1 = xv[1] * yv[1], s2 = xv[2] * yv[2];
 #pragma unroll
                 for (int e = 3; e < 9; e += 3) {
                     s0 = fma(xv[e], yv[e], s0); s1 = fma(xv[e + 1], yv[e + 1], s1); s2 = fma(xv[e + 2], yv[e + 2], s2);
                 }
-                vb[j * 9 + lane] = bj - (s0 + s1 + s2);
+                vb[j * 9 + l] = bj - (s0 + s1 + s2);
             }
             wave_sync();
         }
@@ -1006,40 +1047,41 @@ __device__ void tw_solve_meet(const T *Ii, const T *Xs, int NB, int m, LdsT<T> *
 }
 template <typename T>
 __device__ void tw_solve_back(const T *Ii, const T *Xs, int NB, int m, LdsT<T> *vb, LdsT<T> *ring) {
-    const int lane = threadIdx.x & 63;
-    const bool top = (threadIdx.x >> 6) == 0;
-    const int lr = lane < 9 ? lane : 0;
+    const int lane = threadIdx.x & 63, l = lane & 31;
+    const bool top = lane < 32;
+    const int lr = l < 9 ? l : 0;
     // step i: top j = m - 1 - i (I_j, X_{j+1} at So[j]); bottom j = m + 1 + i (I_j, Y_{j-1} at So[j-1])
-    const int n = top ? m : NB - 1 - m;
-    ChunkStream<T, KB> I{Ii + (size_t)(top ? m - 1 : m + 1) * 81, top ? -81L : 81L, n, ring, {}, {}};
-    ChunkStream<T, KB> X{Xs + (size_t)(top ? m - 1 : m) * 81, top ? -81L : 81L, n, ring + 2 * KB * RSLOT, {}, {}};
+    const int n = top ? m : NB - 1 - m, nmax = m;
+    ChunkStream<T, KB> I{Ii + (size_t)(top ? m - 1 : m + 1) * 81, top ? -81L : 81L, n > 0 ? n : 1, ring, {}};
+    ChunkStream<T, KB> X{Xs + (size_t)(top ? m - 1 : m) * 81, top ? -81L : 81L, n > 0 ? n : 1, ring + 2 * KB * RSLOT, {}};
     I.issue(0);
     X.issue(0);
     I.land(0);
     X.land(0);
-    for (int c = 0; c * KB < n; ++c) {
+    for (int c = 0; c * KB < nmax; ++c) {
         I.issue(c + 1);
         X.issue(c + 1);
         wave_sync();
         for (int q = 0; q < KB; ++q) {
             const int i = c * KB + q;
-            if (i >= n) break;
+            if (i >= nmax) break;
             const int j = top ? m - 1 - i : m + 1 + i, jn = top ? j + 1 : j - 1;
             T v = T(0);
-            if (lane < 9) {
+            const bool act = l < 9 && i < n;
+            if (act) {
                 const LdsT<T> *ir = I.blk(i) + lr * 9;    // symmetric: row == column
                 const LdsT<T> *xb = X.blk(i);
-                const LdsT<T> *y = vb + j * 9, *xn = vb + jn * 9;
+                const LdsT<T> *yv_ = vb + j * 9, *xn = vb + jn * 9;
                 T iv[9], yv[9], xc[9], nv[9];
 #pragma unroll
-                for (int e = 0; e < 9; ++e) { iv[e] = ir[e]; yv[e] = y[e]; xc[e] = xb[e * 9 + lr]; nv[e] = xn[e]; }
+                for (int e = 0; e < 9; ++e) { iv[e] = ir[e]; yv[e] = yv_[e]; xc[e] = xb[e * 9 + lr]; nv[e] = xn[e]; }
                 T s0 = iv[0] * yv[0], s1 = -(xc[0] * nv[0]);
 #pragma unroll
                 for (int e = 1; e < 9; ++e) { s0 = fma(iv[e], yv[e], s0); s1 = fma(-xc[e], nv[e], s1); }
                 v = s0 + s1;
             }
             wave_sync();
-            if (lane < 9) vb[j * 9 + lane] = v;
+            if (act) vb[j * 9 + l] = v;
             wave_sync();
         }
         I.land(c + 1);
@@ -1355,7 +1397,7 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
     // dynamic LDS: the (N+2) x 9 Schur vector, then two block rings per wave for the sweeps
     LdsT<T> *shl = (LdsT<T> *)sh;
     C.vb = (LdsT<T> *)reinterpret_cast<T *>(dsmem);
-    LdsT<T> *ring = C.vb + ((NB * 9 + 7) & ~7) + (tid >> 6) * SWEEP_LDS;
+    LdsT<T> *ring = C.vb + ((NB * 9 + 7) & ~7) + (tid >> 5) * SWEEP_LDS;   // per half-wave
     C.Sd = C.ws + Ws<ROBOT>::Sd;
     C.So = C.ws + Ws<ROBOT>::So;
 #ifdef CMPC_STAMPS
@@ -1434,9 +1476,9 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
         STAMP(2);
         // ---- factorization of S with the predictor's forward elimination fused in
 #ifdef CMPC_STAMPS
-        if (tid < 128) tw_factor_ends<T>(C.Sd, C.So, NB, NBm, shl, C.vb, d.stamps + (size_t)b * 16);
+        tw_factor_ends<T>(C.Sd, C.So, NB, NBm, shl, C.vb, d.stamps + (size_t)b * 16);
 #else
-        if (tid < 128) tw_factor_ends<T>(C.Sd, C.So, NB, NBm, shl, C.vb, nullptr);
+        tw_factor_ends<T>(C.Sd, C.So, NB, NBm, shl, C.vb, nullptr);
 #endif
         __syncthreads();
         if (tid < 64) tw_factor_meet<T>(C.Sd, C.So, NBm, shl, C.vb);
@@ -1453,12 +1495,12 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
                 for (int k = tid; k < K1; k += NT) phase_rhs<T, ROBOT>(C, k);
                 __syncthreads();
                 STAMP(5);
-                if (tid < 128) tw_solve_elim<T>(C.So, NB, NBm, C.vb, ring);
+                tw_solve_elim<T>(C.So, NB, NBm, C.vb, ring);
                 __syncthreads();
                 if (tid < 64) tw_solve_meet<T>(C.Sd, C.So, NB, NBm, C.vb, shl);
                 __syncthreads();
             }
-            if (tid < 128) tw_solve_back<T>(C.Sd, C.So, NB, NBm, C.vb, ring);
+            tw_solve_back<T>(C.Sd, C.So, NB, NBm, C.vb, ring);
             __syncthreads();
             STAMP(6);
             T am[1] = {T(1)}, mus[3] = {T(0), T(0), T(0)};
@@ -1521,7 +1563,7 @@ INST(float, 1)
 #undef INST
 
 size_t ipm_lds_bytes(int N, int prec_bytes) {
-    return ((((size_t)(N + 2) * 9 + 7) & ~size_t(7)) + (size_t)(IPM_NT / 64) * SWEEP_LDS) * prec_bytes;
+    return ((((size_t)(N + 2) * 9 + 7) & ~size_t(7)) + (size_t)2 * SWEEP_LDS) * prec_bytes;
 }
 
 size_t ipm_workspace_elems(int N, int robot) {
