@@ -35,10 +35,11 @@
 namespace cmpc {
 
 constexpr int NT = IPM_NT;   // one wave: a half-wave per end of the Schur sweeps; knots k, k + 64, ...
-constexpr int FU = 34;   // per-contact factor record: Gw 12 | Kinv 10 | F 6 | Winvd 6
-// per-knot (x, t) factor record: 1/Wx[0:6] | M_LL packed 6 | chol(K_TR) packed 36 (diagonal as 1/L_jj) | z1 = L^-1 1 (8) |
-// 1/den | D_slack  (K_TR = D_TR^-1 + G_L W_L^-1 G_L', see phase_factor)
-constexpr int FX = 64, FX_ML = 6, FX_L = 12, FX_Z1 = 48, FX_DEN = 56, FX_DSL = 57;
+// Stored parts of the Phi factors (phase_factor -> phase_sblock, phi_solve_u); the rest (the
+// trust-region Cholesky factor, each contact's G W^-1 and Kinv) is recomputed in registers by the
+// phases that use it (tr_factor, fric_factor), which costs less than its HBM round trip.
+constexpr int FU = 12, FU_F = 0, FU_WI = 6;   // per contact: F = [Phi_u^-1] force block, packed 6 | 1 / W' diagonal 6
+constexpr int FX = 6, FX_ML = 0;               // per knot: M_LL = [Phi^-1]_LL packed 6
 
 // Workspace of one problem.  Per-knot arrays and the per-block vectors (nu, r_e; block j in
 // column j) are field rows of pitch KPC (field-major, see the layout note above); their offsets
@@ -291,6 +292,75 @@ template <typename T> __device__ void chol8(T (&a)[36]) {
     }
 }
 
+// (L, t) block factor of knot k from its trust-region and slack rows (s, lambda of rows 0..8):
+//   K = D_TR^-1 + Y G_L' (8x8 SPD; Y = G_L W_L^-1; D^-1 floored: at a vertex of the trust
+//   region more than 3 rows are active and K -> rank 3),  L L' = K (packed, 1 / L_jj on the
+//   diagonal),  z1 = L^-1 1,  D_sl = lambda_8 / s_8,  1 / den = 1 / (D_sl + cw^2 |z1|^2).
+// Recomputed in registers by every phase that needs it: cheaper than an HBM round trip.
+template <typename T, int ROBOT>
+__device__ __forceinline__ void tr_factor(const Ctx<T, ROBOT> &C, const T *s, const T *lm, T (&Lk)[36], T (&z1)[8],
+                                          T &iden, T &dsl) {
+    const DevParams<T> &P = *C.prm;
+    const T wl[3] = {T(1) / P.Wx[6], T(1) / P.Wx[7], T(1) / P.Wx[8]};
+    const T kfl = T(KFLOOR<T>) * T(8) * (wl[0] + wl[1] + wl[2]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int q = 0; q <= j; ++q) {
+            T v = T(0);
+            for (int i = 0; i < 3; ++i) v += tr_sign<T>(j, i) * tr_sign<T>(q, i) * wl[i];
+            if (q == j) v += fmax(fdiv(s[j], lm[j]), kfl);
+            Lk[j * (j + 1) / 2 + q] = v;
+        }
+    chol8(Lk);
+    T kap = T(0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        T a1 = T(1);
+        for (int q = 0; q < j; ++q) a1 -= Lk[j * (j + 1) / 2 + q] * z1[q];
+        z1[j] = a1 * Lk[j * (j + 1) / 2 + j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) kap += z1[j] * z1[j];
+    dsl = fdiv(lm[8], s[8]);
+    iden = rcp_nr(dsl + C.cw * C.cw * kap);
+}
+
+// friction block of one contact (4 pyramid rows, s4 / l4 their slacks and multipliers):
+// Gw = G W^-1 (4x3) and Kinv = (D^-1 + G W^-1 G')^-1 (packed), with a floor on D^-1 relative to
+// tr(G W^-1 G') (at a zero force all four rows are active and K -> rank 3).  Inactive contacts:
+// Gw = 0, Kinv = I, so (with rhat = 0 on their rows) they contribute nothing.
+template <typename T>
+__device__ __forceinline__ void fric_factor(const T (&G)[12], const T (&wi)[3], const T *s4, const T *l4, bool act,
+                                            T (&Gw)[4][3], T (&Ki)[10]) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) Gw[r][q] = G[3 * r + q] * wi[q];
+    T Km[4][4], tr = T(0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            T acc = T(0);
+            for (int z = 0; z < 3; ++z) acc += Gw[r][z] * G[3 * q + z];
+            Km[r][q] = acc;
+        }
+    for (int r = 0; r < 4; ++r) tr += Km[r][r];
+    const T kfloor = T(KFLOOR<T>) * tr + T(sizeof(T) == 8 ? 1e-300 : 1e-37);
+    for (int r = 0; r < 4; ++r) Km[r][r] += fmax(fdiv(s4[r], act ? l4[r] : T(1)), kfloor);
+    inv4spd(Km, Ki);
+    // masking by arithmetic (every value is finite: lambda -> 1 on inactive rows); per-lane
+    // selects here make the compiler split the contact code into divergent regions
+    const T on = act ? T(1) : T(0), off = T(1) - on;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) Gw[r][q] *= on;
+#pragma unroll
+    for (int q = 0; q < 10; ++q) Ki[q] = (q == 0 || q == 2 || q == 5 || q == 9) ? fma(Ki[q], on, off) : Ki[q] * on;
+}
+
 // ------------------------------------------------------------------ phases
 // (1) residuals of knot k; returns norm contributions
 template <typename T, int ROBOT> struct Norms { T prim, dual, comp, mu, sp, sd, lmax, cnt; };
@@ -423,99 +493,61 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_factor(const C
             for (int e = 0; e < 12; ++e) Gr[c][e] = st[S::CON + S::CS * c + S::G + e];
     }
     const SV<T> fx = C.kv(WF(facx), k);
-    // (L, t) block in push-through form (no D * r product, no cancellation as rows pin L or t):
-    //   K = D_TR^-1 + Y G_L' (8x8 SPD; Y = G_L W_L^-1; D^-1 floored: at a vertex of the trust
-    //   region more than 3 rows are active and K -> rank 3),  L L' = K,  z1 = L^-1 1,
-    //   den = D_slack + cw^2 |z1|^2,  Z = L^-1 Y,  g = Z' z1,
-    //   M_LL = [Phi^-1]_LL = W_L^-1 - Z'Z + cw^2 g g' / den
+    // (L, t) block in push-through form (no D * r product, no cancellation as rows pin L or t),
+    // see tr_factor; stored: M_LL = [Phi^-1]_LL = W_L^-1 - Z'Z + cw^2 g g' / den with
+    // Z = L^-1 Y, g = Z' z1 (phase_sblock).  L, z1, den are recomputed where they are used.
     const T wl[3] = {T(1) / P.Wx[6], T(1) / P.Wx[7], T(1) / P.Wx[8]};
-    const T kfl = T(KFLOOR<T>) * T(8) * (wl[0] + wl[1] + wl[2]);
-    T Lk[36];
-    for (int j = 0; j < 8; ++j)
-        for (int q = 0; q <= j; ++q) {
-            T v = T(0);
-            for (int i = 0; i < 3; ++i) v += tr_sign<T>(j, i) * tr_sign<T>(q, i) * wl[i];
-            if (q == j) v += fmax(fdiv(s[j], lm[j]), kfl);
-            Lk[j * (j + 1) / 2 + q] = v;
-        }
-    chol8(Lk);
-    T z1[8], Z[8][3];
+    T Lk[36], z1[8], iden, dsl;
+    tr_factor(C, s, lm, Lk, z1, iden, dsl);
+    T Z[8][3];
     for (int j = 0; j < 8; ++j) {
-        T a1 = T(1), az[3];
+        T az[3];
         for (int i = 0; i < 3; ++i) az[i] = tr_sign<T>(j, i) * wl[i];
         for (int q = 0; q < j; ++q) {
             const T l = Lk[j * (j + 1) / 2 + q];
-            a1 -= l * z1[q];
             for (int i = 0; i < 3; ++i) az[i] -= l * Z[q][i];
         }
         const T il = Lk[j * (j + 1) / 2 + j];
-        z1[j] = a1 * il;
         for (int i = 0; i < 3; ++i) Z[j][i] = az[i] * il;
     }
-    T kap = T(0), g[3] = {0, 0, 0};
-    for (int j = 0; j < 8; ++j) {
-        kap += z1[j] * z1[j];
+    T g[3] = {0, 0, 0};
+    for (int j = 0; j < 8; ++j)
         for (int i = 0; i < 3; ++i) g[i] += Z[j][i] * z1[j];
-    }
-    const T dsl = fdiv(lm[8], s[8]);
-    const T iden = rcp_nr(dsl + C.cw * C.cw * kap);
-    for (int i = 0; i < 6; ++i) fx[i] = T(1) / P.Wx[i];
     for (int i = 0, p = 0; i < 3; ++i)
         for (int q = 0; q <= i; ++q, ++p) {
             T zz = T(0);
             for (int j = 0; j < 8; ++j) zz += Z[j][i] * Z[j][q];
             fx[FX_ML + p] = (i == q ? wl[i] : T(0)) - zz + C.cw * C.cw * g[i] * g[q] * iden;
         }
-    for (int e = 0; e < 36; ++e) fx[FX_L + e] = Lk[e];
-    for (int j = 0; j < 8; ++j) fx[FX_Z1 + j] = z1[j];
-    fx[FX_DEN] = iden;
-    fx[FX_DSL] = dsl;
     if (k >= N) return;
+#pragma unroll
     for (int c = 0; c < NC; ++c) {
         const SV<T> fu = C.kv(WF(facu), k) + c * FU;
         const T *Wc = P.Wu + NUPC * c;
         const bool act = (msk >> c) & 1u;
         // Winvd: inverse diagonal of W' (CoP rows fold into their coordinate's diagonal)
-        for (int q = 0; q < NUPC; ++q) fu[28 + q] = T(1) / Wc[q];
+        for (int q = 0; q < NUPC; ++q) fu[FU_WI + q] = T(1) / Wc[q];
         if (ROBOT == 1 && act) {
             for (int dd = 0; dd < 2; ++dd) {
                 const int r0 = R_::CP + 4 * c + 2 * dd;
-                fu[28 + dd] = T(1) / (Wc[dd] + C.Dform(lm[r0], s[r0]) + C.Dform(lm[r0 + 1], s[r0 + 1]));
+                fu[FU_WI + dd] = T(1) / (Wc[dd] + C.Dform(lm[r0], s[r0]) + C.Dform(lm[r0 + 1], s[r0 + 1]));
             }
         }
         const T wi[3] = {T(1) / Wc[FO], T(1) / Wc[FO + 1], T(1) / Wc[FO + 2]};
         if (!act) {
-            for (int q = 0; q < 12; ++q) fu[q] = T(0);
-            for (int q = 0; q < 10; ++q) fu[12 + q] = T(0);
-            fu[12 + 0] = fu[12 + 2] = fu[12 + 5] = fu[12 + 9] = T(1);
-            fu[22] = wi[0]; fu[23] = T(0); fu[24] = wi[1]; fu[25] = T(0); fu[26] = T(0); fu[27] = wi[2];
+            fu[FU_F] = wi[0]; fu[FU_F + 1] = T(0); fu[FU_F + 2] = wi[1]; fu[FU_F + 3] = T(0); fu[FU_F + 4] = T(0); fu[FU_F + 5] = wi[2];
             continue;
         }
-        T Gw[4][3];
-        for (int r = 0; r < 4; ++r)
-            for (int q = 0; q < 3; ++q) { Gw[r][q] = Gr[c][3 * r + q] * wi[q]; fu[3 * r + q] = Gw[r][q]; }
-        T Km[4][4], tr = T(0);
-        for (int r = 0; r < 4; ++r)
-            for (int q = 0; q < 4; ++q) {
-                T acc = T(0);
-                for (int z = 0; z < 3; ++z) acc += Gw[r][z] * Gr[c][3 * q + z];
-                Km[r][q] = acc;
-            }
-        for (int r = 0; r < 4; ++r) tr += Km[r][r];
-        // floor on D^-1: at a zero force all four pyramid rows are active (K -> rank 3)
-        const T kfloor = T(KFLOOR<T>) * tr + T(sizeof(T) == 8 ? 1e-300 : 1e-37);
-        for (int r = 0; r < 4; ++r) Km[r][r] += fmax(fdiv(s[R_::FR + 4 * c + r], lm[R_::FR + 4 * c + r]), kfloor);
-        T Ki[10];
-        inv4spd(Km, Ki);
-        for (int q = 0; q < 10; ++q) fu[12 + q] = Ki[q];
-        // F = W^-1 - Gw' Kinv Gw
+        T Gw[4][3], Ki[10];
+        fric_factor(Gr[c], wi, s + R_::FR + 4 * c, lm + R_::FR + 4 * c, true, Gw, Ki);
+        // F = W^-1 - Gw' Kinv Gw  (stored for phi_solve_u and phase_sblock)
         int p = 0;
         for (int i = 0; i < 3; ++i)
             for (int j = 0; j <= i; ++j) {
                 T acc = (i == j) ? wi[i] : T(0);
                 for (int r = 0; r < 4; ++r)
                     for (int q = 0; q < 4; ++q) acc -= Gw[r][i] * Ki[p4(r, q)] * Gw[q][j];
-                fu[22 + p++] = acc;
+                fu[FU_F + p++] = acc;
             }
     }
 }
@@ -527,9 +559,9 @@ template <typename T, int ROBOT> __device__ void phi_solve_u(const Ctx<T, ROBOT>
         const SV<T> fu = C.kv(WF(facu), k) + c * FU;
         const T *vc = vu + NUPC * c;
         T *oc = ou + NUPC * c;
-        for (int q = 0; q < NUPC; ++q) oc[q] = fu[28 + q] * vc[q];
+        for (int q = 0; q < NUPC; ++q) oc[q] = fu[FU_WI + q] * vc[q];
         T F[6];
-        ldv(fu + 22, F);
+        ldv(fu + FU_F, F);
         for (int i = 0; i < 3; ++i)
             oc[FO + i] = sym3(F, i, 0) * vc[FO] + sym3(F, i, 1) * vc[FO + 1] + sym3(F, i, 2) * vc[FO + 2];
     }
@@ -541,12 +573,8 @@ template <typename T, int ROBOT> __device__ void phi_solve_u(const Ctx<T, ROBOT>
 // dt = (vt + D_sl rh_8 - cw z1'y) / den with y = L^-1 (Y vL + rh);  dlam = L^-T (y + cw dt z1);
 // dL = W_L^-1 (vL - G_L' dlam);  dlam_sl = cw 1'dlam - vt  (the t row of the dual residual)
 template <typename T, int ROBOT>
-__device__ void tr_local(const Ctx<T, ROBOT> &C, int k, const T *vL, T vt, const T *rh, T *dL, T &dt, T *dlt, T &dls) {
-    const SV<T> fx = C.kv(WF(facx), k);
-    T Lk[36], z1[8];
-    ldv(fx + FX_L, Lk);
-    ldv(fx + FX_Z1, z1);
-    const T fdsl = fx[FX_DSL], fden = fx[FX_DEN];
+__device__ __forceinline__ void tr_local(const Ctx<T, ROBOT> &C, const T (&Lk)[36], const T (&z1)[8], T fdsl, T fden,
+                                         const T *vL, T vt, const T *rh, T *dL, T &dt, T *dlt, T &dls) {
     const T wl[3] = {rcp_nr(C.prm->Wx[6]), rcp_nr(C.prm->Wx[7]), rcp_nr(C.prm->Wx[8])};
     T y[8];
     for (int j = 0; j < 8; ++j) {
@@ -583,8 +611,13 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_sblock(const C
     const bool hu = k < N;
     // loads: M_k, M_{k+1} (1/Wx[0:6] | M_LL packed), the stage's A/B data, the contacts' F, W'^-1
     T f0[12], f1[12];
-    ldv(C.kv(WF(facx), k), f0);
-    ldv(C.kv(WF(facx), hu ? k + 1 : k), f1);
+    for (int i = 0; i < 6; ++i) f0[i] = f1[i] = T(1) / C.prm->Wx[i];
+    {
+        T m0[6], m1[6];
+        ldv(C.kv(WF(facx), k) + FX_ML, m0);
+        ldv(C.kv(WF(facx), hu ? k + 1 : k) + FX_ML, m1);
+        for (int i = 0; i < 6; ++i) { f0[6 + i] = m0[i]; f1[6 + i] = m1[i]; }
+    }
     const auto st = C.st(k);
     T w[3], w1[3];
     ldv(st + S::W, w);
@@ -595,8 +628,8 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_sblock(const C
         al[c] = hu ? cs[S::ALPHA] : T(0);
         ldv(cs + S::LEVER, lev[c]);
         const SV<T> fu = C.kv(WF(facu), k) + c * FU;
-        ldv(fu + 22, F[c]);
-        ldv(fu + 28, wd[c]);
+        ldv(fu + FU_F, F[c]);
+        ldv(fu + FU_WI, wd[c]);
     }
     T bc[NC][6], bt[NC][3];
     if (ROBOT == 1)
@@ -1092,9 +1125,9 @@ __device__ void tw_solve_back(const T *Ii, const T *Xs, int NB, int m, LdsT<T> *
 
 // r_hat = r_i - r_c / lambda for the rows of knot k  (rc supplied per mode)
 template <typename T, int ROBOT>
-__device__ void rhat_rows(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu, T *rh) {
+__device__ void rhat_rows(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu, const T *s, const T *lm, T *rh) {
     constexpr int NI = Rows<ROBOT>::NI;
-    const SV<T> s = C.kv(WF(s), k), lm = C.kv(WF(l), k), rdi = C.kv(WF(rdi), k);
+    const SV<T> rdi = C.kv(WF(rdi), k);
     const SV<T> dsa = C.kv(WF(dsa), k), dla = C.kv(WF(dla), k);
     const unsigned msk = C.cmask(k);
     for (int r = 0; r < NI; ++r) {
@@ -1109,23 +1142,29 @@ __device__ void rhat_rows(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu, T
 
 // (5a) particular solution w = Phi^-1 (r_d + G' D rhat) (friction rows in push-through form)
 template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_w(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu) {
+    using S = Stage<ROBOT>;
     using R_ = Rows<ROBOT>;
     constexpr int NI = R_::NI, NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
     const int N = C.N;
     const bool hu = k < N;
+    const DevParams<T> &P = *C.prm;
+    T sv[NI], lv[NI];
+    ldv(C.kv(WF(s), k), sv);
+    ldv(C.kv(WF(l), k), lv);
     T rh[NI];
-    rhat_rows(C, k, corr, sigma_mu, rh);   // kept for phase_dz (stored below)
-    T rdx[9], fxd[6], rdu[NU];
+    rhat_rows(C, k, corr, sigma_mu, sv, lv, rh);   // kept for phase_dz (stored below)
+    T rdx[9], rdu[NU];
     ldv(C.kv(WF(rdx), k), rdx);
-    ldv(C.kv(WF(facx), k), fxd);
     ldv(C.kv(WF(rdu), k), rdu);   // k = N: unused
     const T rdt = C.kv(WF(rdt), k)[0];
     T wx[9], wt;
-    for (int i = 0; i < 6; ++i) wx[i] = fxd[i] * rdx[i];
+    for (int i = 0; i < 6; ++i) wx[i] = (T(1) / P.Wx[i]) * rdx[i];
     {   // (L, t): w = -(local solve with v = -r_d)
+        T Lk[36], z1[8], iden, dsl;
+        tr_factor(C, sv, lv, Lk, z1, iden, dsl);
         const T vL[3] = {-rdx[6], -rdx[7], -rdx[8]};
         T dL[3], dt, dlt[8], dls;
-        tr_local(C, k, vL, -rdt, rh, dL, dt, dlt, dls);
+        tr_local(C, Lk, z1, dsl, iden, vL, -rdt, rh, dL, dt, dlt, dls);
         for (int i = 0; i < 3; ++i) wx[6 + i] = -dL[i];
         wt = -dt;
     }
@@ -1134,27 +1173,32 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_w(const Ctx<T,
         T vu[NU];
         for (int i = 0; i < NU; ++i) vu[i] = rdu[i];
         if (ROBOT == 1) {   // CoP rows (D-form, folded into W_cop); absent rows: lambda = 0 -> D = 0, rhat = 0
-            const SV<T> s = C.kv(WF(s), k), lm = C.kv(WF(l), k);
             for (int c = 0; c < NC; ++c)
                 for (int dd = 0; dd < 2; ++dd) {
                     const int r0 = R_::CP + 4 * c + 2 * dd;
-                    vu[NUPC * c + dd] += C.Dform(lm[r0], s[r0]) * rh[r0] - C.Dform(lm[r0 + 1], s[r0 + 1]) * rh[r0 + 1];
+                    vu[NUPC * c + dd] += C.Dform(lv[r0], sv[r0]) * rh[r0] - C.Dform(lv[r0 + 1], sv[r0 + 1]) * rh[r0 + 1];
                 }
         }
         phi_solve_u(C, k, vu, ou);
+        const auto st = C.st(k);
+        const unsigned msk = C.cmask(k);
+#pragma unroll
         for (int c = 0; c < NC; ++c) {
-            // inactive contacts: Gw = 0, Kinv = I and rhat = 0, so they contribute nothing
-            T g[22];
-            ldv(C.kv(WF(facu), k) + c * FU, g);
+            T G[12];
+            ldv(st + (S::CON + S::CS * c + S::G), G);
+            const T *Wc = P.Wu + NUPC * c;
+            const T wi[3] = {T(1) / Wc[FO], T(1) / Wc[FO + 1], T(1) / Wc[FO + 2]};
+            T Gw[4][3], Ki[10];
+            fric_factor(G, wi, sv + R_::FR + 4 * c, lv + R_::FR + 4 * c, (msk >> c) & 1u, Gw, Ki);
             T kr[4];
             for (int r = 0; r < 4; ++r) {
                 T acc = T(0);
-                for (int q = 0; q < 4; ++q) acc += g[12 + p4(r, q)] * rh[R_::FR + 4 * c + q];
+                for (int q = 0; q < 4; ++q) acc += Ki[p4(r, q)] * rh[R_::FR + 4 * c + q];
                 kr[r] = acc;
             }
             for (int i = 0; i < 3; ++i) {
                 T acc = T(0);
-                for (int r = 0; r < 4; ++r) acc += g[3 * r + i] * kr[r];
+                for (int r = 0; r < 4; ++r) acc += Gw[r][i] * kr[r];
                 ou[NUPC * c + FO + i] += acc;
             }
         }
@@ -1199,10 +1243,9 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_rhs(const Ctx<
 template <typename T, int ROBOT>
 __device__ __forceinline__ T dz_rows(const Ctx<T, ROBOT> &C, int k, const T (&dx)[9], T dtt, const T (&du)[NU],
                                      const T (&eu)[NU], const T (&dlt)[8], T dls, const T (&rh)[Rows<ROBOT>::NI],
-                                     const int ld, const T *__restrict__ st, const T *__restrict__ fu,
-                                     const T *__restrict__ rdu, const T *__restrict__ rdi,
-                                     const T *__restrict__ sv, const T *__restrict__ lm, T *__restrict__ ds,
-                                     T *__restrict__ dl, T (&mus)[3]) {
+                                     const T (&sv)[Rows<ROBOT>::NI], const T (&lm)[Rows<ROBOT>::NI],
+                                     const int ld, const T *__restrict__ st, const T *__restrict__ rdu,
+                                     const T *__restrict__ rdi, T *__restrict__ ds, T *__restrict__ dl, T (&mus)[3]) {
     using S = Stage<ROBOT>;
     using R_ = Rows<ROBOT>;
     constexpr int NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
@@ -1213,7 +1256,7 @@ __device__ __forceinline__ T dz_rows(const Ctx<T, ROBOT> &C, int k, const T (&dx
         const T dsr = pr ? -rdi[r * ld] - g : T(0);
         ds[r * ld] = dsr;
         dl[r * ld] = dlr;
-        const T sr = sv[r * ld], lr = lm[r * ld];
+        const T sr = sv[r], lr = lm[r];
         // sum_r (s + a ds)(lambda + a dl) = mus0 + a mus1 + a^2 mus2 (absent rows: lambda = ds = dl = 0)
         mus[0] = fma(sr, lr, mus[0]);
         mus[1] = fma(sr, dlr, fma(lr, dsr, mus[1]));
@@ -1231,18 +1274,21 @@ __device__ __forceinline__ T dz_rows(const Ctx<T, ROBOT> &C, int k, const T (&dx
     for (int c = 0; c < NC; ++c) {
         const bool pr = hu && ((msk >> c) & 1u);
         const T *cs = st + (S::CON + S::CS * c) * ld;
-        const T *g = fu + c * FU * ld;
+        T G[12];
+        for (int e = 0; e < 12; ++e) G[e] = cs[(S::G + e) * ld];
+        const T *Wc = C.prm->Wu + NUPC * c;
+        const T wi[3] = {T(1) / Wc[FO], T(1) / Wc[FO + 1], T(1) / Wc[FO + 2]};
+        T Gw[4][3], Ki[10];
+        fric_factor(G, wi, sv + R_::FR + 4 * c, lm + R_::FR + 4 * c, pr, Gw, Ki);
         T vf[3];
         for (int i = 0; i < 3; ++i) vf[i] = hu ? -(rdu[(NUPC * c + FO + i) * ld] + eu[NUPC * c + FO + i]) : T(0);
         T z[4];
         for (int r = 0; r < 4; ++r)
-            z[r] = g[(3 * r) * ld] * vf[0] + g[(3 * r + 1) * ld] * vf[1] + g[(3 * r + 2) * ld] * vf[2] +
-                   rh[R_::FR + 4 * c + r];
+            z[r] = Gw[r][0] * vf[0] + Gw[r][1] * vf[1] + Gw[r][2] * vf[2] + rh[R_::FR + 4 * c + r];
         for (int r = 0; r < 4; ++r) {
             T acc = T(0);
-            for (int q = 0; q < 4; ++q) acc += g[(12 + p4(r, q)) * ld] * z[q];
-            const T gr = cs[(S::G + 3 * r) * ld] * du[NUPC * c + FO] + cs[(S::G + 3 * r + 1) * ld] * du[NUPC * c + FO + 1] +
-                         cs[(S::G + 3 * r + 2) * ld] * du[NUPC * c + FO + 2];
+            for (int q = 0; q < 4; ++q) acc += Ki[p4(r, q)] * z[q];
+            const T gr = G[3 * r] * du[NUPC * c + FO] + G[3 * r + 1] * du[NUPC * c + FO + 1] + G[3 * r + 2] * du[NUPC * c + FO + 2];
             emit(R_::FR + 4 * c + r, pr, gr, hu ? acc : T(0));
         }
     }
@@ -1253,7 +1299,7 @@ __device__ __forceinline__ T dz_rows(const Ctx<T, ROBOT> &C, int k, const T (&dx
             for (int q = 0; q < 4; ++q) {
                 const int r = R_::CP + 4 * c + q, dd = q / 2;
                 const T gr = (q % 2 == 0) ? du[NUPC * c + dd] : -du[NUPC * c + dd];
-                emit(r, pr, gr, pr ? C.Dform(lm[r * ld], sv[r * ld]) * (gr + rh[r]) : T(0));
+                emit(r, pr, gr, pr ? C.Dform(lm[r], sv[r]) * (gr + rh[r]) : T(0));
             }
         }
     }
@@ -1277,17 +1323,20 @@ __device__ PHASE_ATTR T phase_dz(const Ctx<T, ROBOT> &C, int k, int corr, T (&mu
     opBT<T, ROBOT>(C.st(kc), d1, eu);
     for (int i = 0; i < 9; ++i)
         ex[i] = (k == 0 ? dk[i] : -dk[i]) + (hu ? a[i] : T(0)) + (k == N ? d1[i] : T(0));
-    T rh[NI], rdx[9], fxd[6], wu[NU];
+    T rh[NI], rdx[9], wu[NU], sv[NI], lv[NI];
     ldv(C.kv(WF(rh), k), rh);   // this step's rhat, from phase_w
     ldv(C.kv(WF(rdx), k), rdx);
-    ldv(C.kv(WF(facx), k), fxd);
     ldv(C.kv(WF(wu), kc), wu);
+    ldv(C.kv(WF(s), k), sv);
+    ldv(C.kv(WF(l), k), lv);
     const T rdt = C.kv(WF(rdt), k)[0];
     T dx[9], dtt, du[NU], dlt[8], dls;
-    for (int i = 0; i < 6; ++i) dx[i] = -fxd[i] * (rdx[i] + ex[i]);
+    for (int i = 0; i < 6; ++i) dx[i] = -(T(1) / C.prm->Wx[i]) * (rdx[i] + ex[i]);
     {
+        T Lk[36], z1[8], iden, dsl;
+        tr_factor(C, sv, lv, Lk, z1, iden, dsl);
         const T vL[3] = {-(rdx[6] + ex[6]), -(rdx[7] + ex[7]), -(rdx[8] + ex[8])};
-        tr_local(C, k, vL, -rdt, rh, dx + 6, dtt, dlt, dls);
+        tr_local(C, Lk, z1, dsl, iden, vL, -rdt, rh, dx + 6, dtt, dlt, dls);
     }
     {
         T au[NU];
@@ -1295,9 +1344,9 @@ __device__ PHASE_ATTR T phase_dz(const Ctx<T, ROBOT> &C, int k, int corr, T (&mu
         for (int i = 0; i < NU; ++i) du[i] = hu ? -wu[i] - au[i] : T(0);
     }
     constexpr int ld = KPC;
-    const T amax = dz_rows<T, ROBOT>(C, k, dx, dtt, du, eu, dlt, dls, rh, ld, C.stage + kc,
-                                     C.ws + WF(facu) * KPC + kc, C.ws + WF(rdu) * KPC + kc, C.ws + WF(rdi) * KPC + k,
-                                     C.ws + WF(s) * KPC + k, C.ws + WF(l) * KPC + k, C.ws + (corr ? WF(ds) : WF(dsa)) * KPC + k,
+    const T amax = dz_rows<T, ROBOT>(C, k, dx, dtt, du, eu, dlt, dls, rh, sv, lv, ld, C.stage + kc,
+                                     C.ws + WF(rdu) * KPC + kc, C.ws + WF(rdi) * KPC + k,
+                                     C.ws + (corr ? WF(ds) : WF(dsa)) * KPC + k,
                                      C.ws + (corr ? WF(dl) : WF(dla)) * KPC + k, mus);
     stv(C.kv(WF(dx), k), dx);
     C.kv(WF(dt), k)[0] = dtt;
