@@ -377,101 +377,144 @@ template <int n, typename T, typename P> __device__ __forceinline__ void stv(P p
     for (int i = 0; i < n; ++i) p[i] = v[i];
 }
 
-template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_residual(const Ctx<T, ROBOT> &C, int k, Norms<T, ROBOT> &nm) {
+// The field records are passed as restrict-qualified pointers (field f at p[f * KPC]): loads may
+// then move above the stores, so every result row is stored as soon as it is formed and the
+// phase never holds the whole knot in registers (holding it serialized the loads of late rows
+// behind one memory round trip each).
+template <typename T, int ROBOT>
+__device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<T, ROBOT> &nm, const T *__restrict__ stp,
+                                           const T *__restrict__ xs, const T *__restrict__ us, const T *__restrict__ ts,
+                                           const T *__restrict__ ss, const T *__restrict__ ls, const T *__restrict__ nus,
+                                           T *__restrict__ rdx_o, T *__restrict__ rdt_o, T *__restrict__ rdu_o,
+                                           T *__restrict__ rde_o, T *__restrict__ rdi_o) {
     using S = Stage<ROBOT>;
-    constexpr int NI = Rows<ROBOT>::NI;
+    using R_ = Rows<ROBOT>;
+    constexpr int NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
+    constexpr int ld = KPC;
     const int N = C.N;
     const bool hu = k < N;
     const DevParams<T> &P = *C.prm;
-    const auto st = C.st(k);
-    T x[9], u[NU], sv[NI], lm[NI], nk[9], n1[9], x1[9];
-    ldv(C.var_x(k), x);
-    ldv(C.var_u(k), u);                  // k = N: padding column (values unused)
-    ldv(C.kv(WF(s), k), sv);
-    ldv(C.kv(WF(l), k), lm);
-    ldv(C.bv(WF(nu), k), nk);            // nu block k (k = 0: the initial-state rows)
-    ldv(C.bv(WF(nu), k + 1), n1);        // nu block k+1 (k = N: the final-state rows)
-    ldv(C.var_x(hu ? k + 1 : k), x1);
-    const T t = C.kv(WF(t), k)[0];
+    const SV<const T> st{stp};
     const unsigned msk = C.cmask(k);
-    T lv[NI];
+    T x[9], u[NU];
 #pragma unroll
-    for (int r = 0; r < NI; ++r) lv[r] = Ctx<T, ROBOT>::present_m(msk, r) ? lm[r] : T(0);
-    T gL[3], gt, gu[NU];
-    C.gtv(k, lv, gL, gt, gu);
-    // E' nu at knot k
-    T ex[9], eu[NU];
-    for (int i = 0; i < 9; ++i) ex[i] = (k == 0) ? nk[i] : -nk[i];
-    if (k == N) for (int i = 0; i < 9; ++i) ex[i] += n1[i];
-    if (hu) {
-        T a[9];
-        opAT(st + S::W, C.beta, n1, a);
-        for (int i = 0; i < 9; ++i) ex[i] += a[i];
-        opBT<T, ROBOT>(st, n1, eu);
-    }
-    T rdx[9];
-    for (int i = 0; i < 9; ++i) {
-        const T hx = P.Wx[i] * x[i], q = st[S::QX + i];
-        const T g = (i >= 6) ? gL[i - 6] : T(0);
-        rdx[i] = hx + q + ex[i] + g;
-        nm.dual = fmax(nm.dual, fabs(rdx[i]));
-        nm.sd = fmax(nm.sd, fmax(fabs(hx), fmax(fabs(q), fmax(fabs(ex[i]), fabs(g)))));
-    }
-    const T rdt = T(1) + gt;
-    nm.dual = fmax(nm.dual, fabs(rdt));
-    nm.sd = fmax(nm.sd, T(1));
-    T rdu[NU], rde[9], rdb[9];
-    if (hu) {
-        for (int i = 0; i < NU; ++i) {
-            const T h = P.Wu[i] * u[i];
-            rdu[i] = h + eu[i] + gu[i];
-            nm.dual = fmax(nm.dual, fabs(rdu[i]));
-            nm.sd = fmax(nm.sd, fmax(fabs(h), fmax(fabs(eu[i]), fabs(gu[i]))));
-        }
-        // dynamics row block 1+k
-        T ax[9], bu[9];
-        opA(st + S::W, C.beta, x, ax);
-        opB<T, ROBOT>(st, u, bu);
-        for (int i = 0; i < 9; ++i) {
-            const T ez = ax[i] + bu[i] - x1[i], r = st[S::R + i];
-            rde[i] = ez - r;
-            nm.prim = fmax(nm.prim, fabs(rde[i]));
-            nm.sp = fmax(nm.sp, fmax(fabs(ez), fabs(r)));
-        }
-    }
-    const bool bnd = (k == 0 || k == N);
-    if (bnd) {
-        const T *xb = C.xbar + (size_t)k * 9;
-        for (int i = 0; i < 9; ++i) {
-            rdb[i] = x[i] - xb[i];
-            nm.prim = fmax(nm.prim, fabs(rdb[i]));
-            nm.sp = fmax(nm.sp, fmax(fabs(x[i]), fabs(xb[i])));
-        }
-    }
-    T rdi[NI];
+    for (int i = 0; i < 9; ++i) x[i] = xs[i * ld];
 #pragma unroll
-    for (int r = 0; r < NI; ++r) {
-        const bool pr = Ctx<T, ROBOT>::present_m(msk, r);
-        const T g = C.gz(k, r, x, t, u, false);
-        const T v = C.gz(k, r, x, t, u, true);
-        rdi[r] = pr ? v + sv[r] : T(0);
-        const T c = pr ? sv[r] * lm[r] : T(0);
+    for (int i = 0; i < NU; ++i) u[i] = us[i * ld];   // k = N: padding column (values unused)
+    const T t = ts[0];
+    // inequality rows: r_i = g'z - h + s, complementarity and norms; G' lambda accumulated on the fly
+    T gL[3] = {T(0), T(0), T(0)}, gt = T(0), gu[NU];
+#pragma unroll
+    for (int i = 0; i < NU; ++i) gu[i] = T(0);
+    auto row = [&](int r, bool pr, T g, T h) {
+        const T v = g - h, sr = ss[r * ld], lr = ls[r * ld];
+        rdi_o[r * ld] = pr ? v + sr : T(0);
+        const T c = pr ? sr * lr : T(0);
         nm.prim = fmax(nm.prim, pr ? v : T(0));
         nm.sp = fmax(nm.sp, pr ? fmax(fabs(g), fabs(g - v)) : T(0));
         nm.comp = fmax(nm.comp, c);
         nm.mu += c;
         nm.cnt += pr ? T(1) : T(0);
-        nm.lmax = fmax(nm.lmax, pr ? lm[r] : T(0));
+        nm.lmax = fmax(nm.lmax, pr ? lr : T(0));
+        return pr ? lr : T(0);
+    };
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const T g = tr_sign<T>(j, 0) * x[6] + tr_sign<T>(j, 1) * x[7] + tr_sign<T>(j, 2) * x[8] + C.cw * t;
+        const T lr = row(j, true, g, st[S::BTR + j]);
+        for (int i = 0; i < 3; ++i) gL[i] += tr_sign<T>(j, i) * lr;
+        gt += C.cw * lr;
     }
-    // stores
-    stv(C.kv(WF(rdx), k), rdx);
-    C.kv(WF(rdt), k)[0] = rdt;
+    gt -= row(8, true, -t, T(0));
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const bool pr = hu && ((msk >> c) & 1u);
+        const auto cs = st + (S::CON + S::CS * c);
+        const T *f = u + NUPC * c + FO;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const T g0 = cs[S::G + 3 * r], g1 = cs[S::G + 3 * r + 1], g2 = cs[S::G + 3 * r + 2];
+            const T lr = row(R_::FR + 4 * c + r, pr, g0 * f[0] + g1 * f[1] + g2 * f[2], cs[S::H + r]);
+            gu[NUPC * c + FO] += g0 * lr;
+            gu[NUPC * c + FO + 1] += g1 * lr;
+            gu[NUPC * c + FO + 2] += g2 * lr;
+        }
+        if (ROBOT == 1) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {   // cop <= hi | -cop <= -lo (lo = -(lxn | lyn))
+                const int dd = q / 2;
+                const T cop = u[NUPC * c + dd];
+                const T lr = (q % 2 == 0) ? row(R_::CP + 4 * c + q, pr, cop, P.foot_range[dd == 0 ? 0 : 2])
+                                          : row(R_::CP + 4 * c + q, pr, -cop, P.foot_range[dd == 0 ? 1 : 3]);
+                gu[NUPC * c + dd] += (q % 2 == 0) ? lr : -lr;
+            }
+        }
+    }
+    // E' nu at knot k
+    T nk[9], n1[9], ex[9], eu[NU];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) { nk[i] = nus[i * ld]; n1[i] = nus[i * ld + 1]; }   // nu blocks k, k + 1
+    for (int i = 0; i < 9; ++i) ex[i] = (k == 0) ? nk[i] : -nk[i];
+    if (k == N) for (int i = 0; i < 9; ++i) ex[i] += n1[i];
+    T w[3];
+    for (int i = 0; i < 3; ++i) w[i] = st[S::W + i];
     if (hu) {
-        stv(C.kv(WF(rdu), k), rdu);
-        stv(C.bv(WF(rde), 1 + k), rde);
+        T a[9];
+        opAT(w, C.beta, n1, a);
+        for (int i = 0; i < 9; ++i) ex[i] += a[i];
+        opBT<T, ROBOT>(st, n1, eu);
     }
-    if (bnd) stv(C.bv(WF(rde), k == 0 ? 0 : N + 1), rdb);
-    stv(C.kv(WF(rdi), k), rdi);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        const T hx = P.Wx[i] * x[i], q = st[S::QX + i];
+        const T g = (i >= 6) ? gL[i - 6] : T(0);
+        const T rd = hx + q + ex[i] + g;
+        rdx_o[i * ld] = rd;
+        nm.dual = fmax(nm.dual, fabs(rd));
+        nm.sd = fmax(nm.sd, fmax(fabs(hx), fmax(fabs(q), fmax(fabs(ex[i]), fabs(g)))));
+    }
+    const T rdt = T(1) + gt;
+    rdt_o[0] = rdt;
+    nm.dual = fmax(nm.dual, fabs(rdt));
+    nm.sd = fmax(nm.sd, T(1));
+    if (hu) {
+#pragma unroll
+        for (int i = 0; i < NU; ++i) {
+            const T h = P.Wu[i] * u[i];
+            const T rd = h + eu[i] + gu[i];
+            rdu_o[i * ld] = rd;
+            nm.dual = fmax(nm.dual, fabs(rd));
+            nm.sd = fmax(nm.sd, fmax(fabs(h), fmax(fabs(eu[i]), fabs(gu[i]))));
+        }
+        // dynamics row block 1 + k
+        T ax[9], bu[9];
+        opA(w, C.beta, x, ax);
+        opB<T, ROBOT>(st, u, bu);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            const T ez = ax[i] + bu[i] - xs[i * ld + 1], r = st[S::R + i];   // x_{k+1}
+            const T re = ez - r;
+            rde_o[i * ld + 1 + k] = re;
+            nm.prim = fmax(nm.prim, fabs(re));
+            nm.sp = fmax(nm.sp, fmax(fabs(ez), fabs(r)));
+        }
+    }
+    if (k == 0 || k == N) {   // boundary rows: block 0 (initial state) / N + 1 (final state)
+        const T *xb = C.xbar + (size_t)k * 9;
+        for (int i = 0; i < 9; ++i) {
+            const T rb = x[i] - xb[i];
+            rde_o[i * ld + (k == 0 ? 0 : N + 1)] = rb;
+            nm.prim = fmax(nm.prim, fabs(rb));
+            nm.sp = fmax(nm.sp, fmax(fabs(x[i]), fabs(xb[i])));
+        }
+    }
+}
+
+template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_residual(const Ctx<T, ROBOT> &C, int k, Norms<T, ROBOT> &nm) {
+    T *ws = C.ws;
+    resid_knot<T, ROBOT>(C, k, nm, C.stage + k, ws + WF(x) * KPC + k, ws + WF(u) * KPC + k, ws + WF(t) * KPC + k,
+                         ws + WF(s) * KPC + k, ws + WF(l) * KPC + k, ws + WF(nu) * KPC + k, ws + WF(rdx) * KPC + k,
+                         ws + WF(rdt) * KPC + k, ws + WF(rdu) * KPC + k, ws + WF(rde) * KPC, ws + WF(rdi) * KPC + k);
 }
 
 // (2) Phi factors of knot k
