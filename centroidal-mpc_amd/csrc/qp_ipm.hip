@@ -406,6 +406,9 @@ __device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<
     T gL[3] = {T(0), T(0), T(0)}, gt = T(0), gu[NU];
 #pragma unroll
     for (int i = 0; i < NU; ++i) gu[i] = T(0);
+    // complementarity sums in short per-group chains (one long serial chain made the scheduler
+    // keep every row's product live until the end); the row count is exact in integers
+    T mug = T(0);
     auto row = [&](int r, bool pr, T g, T h) {
         const T v = g - h, sr = ss[r * ld], lr = ls[r * ld];
         rdi_o[r * ld] = pr ? v + sr : T(0);
@@ -413,11 +416,11 @@ __device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<
         nm.prim = fmax(nm.prim, pr ? v : T(0));
         nm.sp = fmax(nm.sp, pr ? fmax(fabs(g), fabs(g - v)) : T(0));
         nm.comp = fmax(nm.comp, c);
-        nm.mu += c;
-        nm.cnt += pr ? T(1) : T(0);
+        mug += c;
         nm.lmax = fmax(nm.lmax, pr ? lr : T(0));
         return pr ? lr : T(0);
     };
+    nm.cnt += T(9 + (hu ? 4 * (1 + Robot<ROBOT>::COP) * __builtin_popcount(msk) : 0));
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const T g = tr_sign<T>(j, 0) * x[6] + tr_sign<T>(j, 1) * x[7] + tr_sign<T>(j, 2) * x[8] + C.cw * t;
@@ -426,8 +429,10 @@ __device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<
         gt += C.cw * lr;
     }
     gt -= row(8, true, -t, T(0));
+    nm.mu += mug;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
+        mug = T(0);
         const bool pr = hu && ((msk >> c) & 1u);
         const auto cs = st + (S::CON + S::CS * c);
         const T *f = u + NUPC * c + FO;
@@ -449,6 +454,7 @@ __device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<
                 gu[NUPC * c + dd] += (q % 2 == 0) ? lr : -lr;
             }
         }
+        nm.mu += mug;
     }
     // E' nu at knot k
     T nk[9], n1[9], ex[9], eu[NU];
