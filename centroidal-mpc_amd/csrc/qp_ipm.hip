@@ -1174,17 +1174,28 @@ __device__ void tw_solve_back(const T *Ii, const T *Xs, int NB, int m, LdsT<T> *
 
 // r_hat = r_i - r_c / lambda for the rows of knot k  (rc supplied per mode)
 template <typename T, int ROBOT>
-__device__ void rhat_rows(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu, const T *s, const T *lm, T *rh) {
+__device__ __forceinline__ void rhat_rows(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu, const T *s, const T *lm,
+                                          T *rh) {
     constexpr int NI = Rows<ROBOT>::NI;
-    const SV<T> rdi = C.kv(WF(rdi), k);
-    const SV<T> dsa = C.kv(WF(dsa), k), dla = C.kv(WF(dla), k);
     const unsigned msk = C.cmask(k);
+    // every row's loads in one batch (a branch per row serialized them)
+    T rd[NI], cc[NI];
+    ldv(C.kv(WF(rdi), k), rd);
+#pragma unroll
+    for (int r = 0; r < NI; ++r) cc[r] = T(0);
+    if (corr) {   // corrector: + ds_aff dlambda_aff - sigma mu
+        T a[NI], b[NI];
+        ldv(C.kv(WF(dsa), k), a);
+        ldv(C.kv(WF(dla), k), b);
+#pragma unroll
+        for (int r = 0; r < NI; ++r) cc[r] = a[r] * b[r] - sigma_mu;
+    }
+#pragma unroll
     for (int r = 0; r < NI; ++r) {
         const bool pr = Ctx<T, ROBOT>::present_m(msk, r);
         const T sr = s[r], lr = lm[r];
-        T rc = sr * lr;
-        if (corr) rc += dsa[r] * dla[r] - sigma_mu;
-        const T v = rdi[r] - fdiv(rc, pr ? lr : T(1));
+        const T rc = sr * lr + cc[r];
+        const T v = rd[r] - fdiv(rc, pr ? lr : T(1));
         rh[r] = pr ? v : T(0);
     }
 }
