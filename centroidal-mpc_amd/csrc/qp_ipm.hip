@@ -1296,27 +1296,41 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_rhs(const Ctx<
 // (5d) direction at knot k from dnu; returns the max step allowed by this knot's rows
 // rows of knot k: ds = -r_i - G dz; dlambda from the push-through solves (TR, slack: dlt, dls;
 // friction: Kinv (Gw v + rhat) with v = -(rdu + E'dnu_u) on the forces) or the D-form (CoP);
-// returns the largest step keeping s, lambda >= 0.  The memory operands are restrict-qualified
-// (field-major records, field f at p[f * ld]) so the loads of s, lambda, r_i, the stage and the
-// friction factors are not held behind the stores of ds, dlambda.  Inactive contacts:
-// G = Gw = 0, Kinv = I, rhat = 0 -> zero steps.
+// returns the largest step keeping s, lambda >= 0, and accumulates the three coefficients of
+// sum_r (s + a ds)(lambda + a dl).  Restrict-qualified field pointers (field f at p[f * KPC]) and
+// contact-by-contact streaming: each row's step is stored as soon as it is formed, so the knot
+// is never held in registers whole.  Inactive contacts: G = Gw = 0, Kinv = I, rhat = 0 -> zero
+// steps.
 template <typename T, int ROBOT>
-__device__ __forceinline__ T dz_rows(const Ctx<T, ROBOT> &C, int k, const T (&dx)[9], T dtt, const T (&du)[NU],
-                                     const T (&eu)[NU], const T (&dlt)[8], T dls, const T (&rh)[Rows<ROBOT>::NI],
-                                     const T (&sv)[Rows<ROBOT>::NI], const T (&lm)[Rows<ROBOT>::NI],
-                                     const int ld, const T *__restrict__ st, const T *__restrict__ rdu,
-                                     const T *__restrict__ rdi, T *__restrict__ ds, T *__restrict__ dl, T (&mus)[3]) {
+__device__ __forceinline__ T dz_knot(const Ctx<T, ROBOT> &C, int k, T (&mus)[3], const T *__restrict__ stp,
+                                     const T *__restrict__ rhp, const T *__restrict__ rdxp, const T *__restrict__ rdtp,
+                                     const T *__restrict__ wup, const T *__restrict__ ss, const T *__restrict__ ls,
+                                     const T *__restrict__ rdip, const T *__restrict__ rdup, const T *__restrict__ fup,
+                                     T *__restrict__ dxo, T *__restrict__ dto, T *__restrict__ duo, T *__restrict__ ds,
+                                     T *__restrict__ dl) {
     using S = Stage<ROBOT>;
     using R_ = Rows<ROBOT>;
     constexpr int NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
-    const bool hu = k < C.N;
+    constexpr int ld = KPC;
+    const int N = C.N;
+    const bool hu = k < N;
+    const SV<const T> st{stp};   // knot kc (= k, or 0 at k = N where no contact row exists)
     const unsigned msk = C.cmask(k);
+    // E' dnu at knot k from the LDS blocks k, k+1 (k = 0: block 0 is the init rows; k = N: block
+    // N+1 the final rows); the knot-type cases are selects (one basic block)
+    const LdsT<T> *vb = C.vb;
+    T dk[9], d1[9], ex[9], eu[NU], a[9], w[3];
+    for (int i = 0; i < 9; ++i) { dk[i] = vb[k * 9 + i]; d1[i] = vb[(k + 1) * 9 + i]; }
+    for (int i = 0; i < 3; ++i) w[i] = st[S::W + i];
+    opAT(w, C.beta, d1, a);
+    opBT<T, ROBOT>(st, d1, eu);
+    for (int i = 0; i < 9; ++i)
+        ex[i] = (k == 0 ? dk[i] : -dk[i]) + (hu ? a[i] : T(0)) + (k == N ? d1[i] : T(0));
     T amax = T(1);
-    auto emit = [&](int r, bool pr, T g, T dlr) {
-        const T dsr = pr ? -rdi[r * ld] - g : T(0);
+    auto emit = [&](int r, bool pr, T g, T dlr, T sr, T lr, T rdir) {
+        const T dsr = pr ? -rdir - g : T(0);
         ds[r * ld] = dsr;
         dl[r * ld] = dlr;
-        const T sr = sv[r], lr = lm[r];
         // sum_r (s + a ds)(lambda + a dl) = mus0 + a mus1 + a^2 mus2 (absent rows: lambda = ds = dl = 0)
         mus[0] = fma(sr, lr, mus[0]);
         mus[1] = fma(sr, dlr, fma(lr, dsr, mus[1]));
@@ -1325,41 +1339,81 @@ __device__ __forceinline__ T dz_rows(const Ctx<T, ROBOT> &C, int k, const T (&dx
         const T qs = fdiv(-sr, dsr < T(0) ? dsr : T(-1)), ql = fdiv(-lr, dlr < T(0) ? dlr : T(-1));
         amax = fmin(amax, fmin(dsr < T(0) ? qs : T(1), dlr < T(0) ? ql : T(1)));
     };
+    // (x, t) part and the trust-region / slack rows
+    {
+        T rdx[9], s9[9], l9[9], rh9[9], ri9[9];
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-        emit(j, true, tr_sign<T>(j, 0) * dx[6] + tr_sign<T>(j, 1) * dx[7] + tr_sign<T>(j, 2) * dx[8] + C.cw * dtt,
-             dlt[j]);
-    emit(8, true, -dtt, dls);
+        for (int i = 0; i < 9; ++i) {
+            rdx[i] = rdxp[i * ld];
+            s9[i] = ss[i * ld];
+            l9[i] = ls[i * ld];
+            rh9[i] = rhp[i * ld];
+            ri9[i] = rdip[i * ld];
+        }
+        const T rdt = rdtp[0];
+        T dx[9], dtt, dlt[8], dls;
+        for (int i = 0; i < 6; ++i) dx[i] = -(T(1) / C.prm->Wx[i]) * (rdx[i] + ex[i]);
+        {
+            T Lk[36], z1[8], iden, dsl;
+            tr_factor(C, s9, l9, Lk, z1, iden, dsl);
+            const T vL[3] = {-(rdx[6] + ex[6]), -(rdx[7] + ex[7]), -(rdx[8] + ex[8])};
+            tr_local(C, Lk, z1, dsl, iden, vL, -rdt, rh9, dx + 6, dtt, dlt, dls);
+        }
+#pragma unroll
+        for (int i = 0; i < 9; ++i) dxo[i * ld] = dx[i];
+        dto[0] = dtt;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            emit(j, true, tr_sign<T>(j, 0) * dx[6] + tr_sign<T>(j, 1) * dx[7] + tr_sign<T>(j, 2) * dx[8] + C.cw * dtt,
+                 dlt[j], s9[j], l9[j], ri9[j]);
+        emit(8, true, -dtt, dls, s9[8], l9[8], ri9[8]);
+    }
+    // contacts, one at a time: du = -w_u - Phi_u^-1 E'dnu_u, then the contact's rows
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         const bool pr = hu && ((msk >> c) & 1u);
-        const T *cs = st + (S::CON + S::CS * c) * ld;
-        T G[12];
-        for (int e = 0; e < 12; ++e) G[e] = cs[(S::G + e) * ld];
+        const T *fu = fup + c * FU * ld;
+        T F[6], wd[NUPC], au[NUPC], du[NUPC];
+        for (int q = 0; q < 6; ++q) F[q] = fu[(FU_F + q) * ld];
+        for (int q = 0; q < NUPC; ++q) wd[q] = fu[(FU_WI + q) * ld];
+        const T *ec = eu + NUPC * c;
+        for (int q = 0; q < NUPC; ++q) au[q] = wd[q] * ec[q];
+        for (int i = 0; i < 3; ++i)
+            au[FO + i] = sym3(F, i, 0) * ec[FO] + sym3(F, i, 1) * ec[FO + 1] + sym3(F, i, 2) * ec[FO + 2];
+        // unconditional loads (kc keeps the addresses valid at k = N) masked by arithmetic: a
+        // select on a loaded value becomes a branch around the load and a wait per row
+        const T hf = hu ? T(1) : T(0);
+        for (int q = 0; q < NUPC; ++q) du[q] = (-wup[(NUPC * c + q) * ld] - au[q]) * hf;
+        if (hu)
+            for (int q = 0; q < NUPC; ++q) duo[(NUPC * c + q) * ld] = du[q];
+        const auto cs = st + (S::CON + S::CS * c);
+        T G[12], s4[4], l4[4], rh4[4], ri4[4], vf[3];
+        for (int e = 0; e < 12; ++e) G[e] = cs[S::G + e];
+        for (int r = 0; r < 4; ++r) {
+            const int row = R_::FR + 4 * c + r;
+            s4[r] = ss[row * ld]; l4[r] = ls[row * ld]; rh4[r] = rhp[row * ld]; ri4[r] = rdip[row * ld];
+        }
+        for (int i = 0; i < 3; ++i) vf[i] = -(rdup[(NUPC * c + FO + i) * ld] + ec[FO + i]) * hf;
         const T *Wc = C.prm->Wu + NUPC * c;
         const T wi[3] = {T(1) / Wc[FO], T(1) / Wc[FO + 1], T(1) / Wc[FO + 2]};
         T Gw[4][3], Ki[10];
-        fric_factor(G, wi, sv + R_::FR + 4 * c, lm + R_::FR + 4 * c, pr, Gw, Ki);
-        T vf[3];
-        for (int i = 0; i < 3; ++i) vf[i] = hu ? -(rdu[(NUPC * c + FO + i) * ld] + eu[NUPC * c + FO + i]) : T(0);
+        fric_factor(G, wi, s4, l4, pr, Gw, Ki);
         T z[4];
-        for (int r = 0; r < 4; ++r)
-            z[r] = Gw[r][0] * vf[0] + Gw[r][1] * vf[1] + Gw[r][2] * vf[2] + rh[R_::FR + 4 * c + r];
+        for (int r = 0; r < 4; ++r) z[r] = Gw[r][0] * vf[0] + Gw[r][1] * vf[1] + Gw[r][2] * vf[2] + rh4[r];
+#pragma unroll
         for (int r = 0; r < 4; ++r) {
             T acc = T(0);
             for (int q = 0; q < 4; ++q) acc += Ki[p4(r, q)] * z[q];
-            const T gr = G[3 * r] * du[NUPC * c + FO] + G[3 * r + 1] * du[NUPC * c + FO + 1] + G[3 * r + 2] * du[NUPC * c + FO + 2];
-            emit(R_::FR + 4 * c + r, pr, gr, hu ? acc : T(0));
+            const T gr = G[3 * r] * du[FO] + G[3 * r + 1] * du[FO + 1] + G[3 * r + 2] * du[FO + 2];
+            emit(R_::FR + 4 * c + r, pr, gr, hu ? acc : T(0), s4[r], l4[r], ri4[r]);
         }
-    }
-    if (ROBOT == 1) {
+        if (ROBOT == 1) {   // CoP rows (D-form)
 #pragma unroll
-        for (int c = 0; c < NC; ++c) {
-            const bool pr = hu && ((msk >> c) & 1u);
             for (int q = 0; q < 4; ++q) {
                 const int r = R_::CP + 4 * c + q, dd = q / 2;
-                const T gr = (q % 2 == 0) ? du[NUPC * c + dd] : -du[NUPC * c + dd];
-                emit(r, pr, gr, pr ? C.Dform(lm[r], sv[r]) * (gr + rh[r]) : T(0));
+                const T sr = ss[r * ld], lr = ls[r * ld];
+                const T gr = (q % 2 == 0) ? du[dd] : -du[dd];
+                emit(r, pr, gr, pr ? C.Dform(lr, sr) * (gr + rhp[r * ld]) : T(0), sr, lr, rdip[r * ld]);
             }
         }
     }
@@ -1368,50 +1422,14 @@ __device__ __forceinline__ T dz_rows(const Ctx<T, ROBOT> &C, int k, const T (&dx
 
 template <typename T, int ROBOT>
 __device__ PHASE_ATTR T phase_dz(const Ctx<T, ROBOT> &C, int k, int corr, T (&mus)[3]) {
-    using S = Stage<ROBOT>;
-    using R_ = Rows<ROBOT>;
-    constexpr int NI = R_::NI;
-    const int N = C.N;
-    const bool hu = k < N;
-    // E' dnu at knot k from the LDS blocks k, k+1 (k = 0: block 0 is the init rows; k = N: block
-    // N+1 the final rows); the knot-type cases are selects (one basic block)
-    const LdsT<T> *vb = C.vb;
-    const int kc = hu ? k : 0;   // k = N: no controls or contacts (stage / factor records unused)
-    T dk[9], d1[9], ex[9], eu[NU], a[9];
-    for (int i = 0; i < 9; ++i) { dk[i] = vb[k * 9 + i]; d1[i] = vb[(k + 1) * 9 + i]; }
-    opAT(C.st(k) + S::W, C.beta, d1, a);
-    opBT<T, ROBOT>(C.st(kc), d1, eu);
-    for (int i = 0; i < 9; ++i)
-        ex[i] = (k == 0 ? dk[i] : -dk[i]) + (hu ? a[i] : T(0)) + (k == N ? d1[i] : T(0));
-    T rh[NI], rdx[9], wu[NU], sv[NI], lv[NI];
-    ldv(C.kv(WF(rh), k), rh);   // this step's rhat, from phase_w
-    ldv(C.kv(WF(rdx), k), rdx);
-    ldv(C.kv(WF(wu), kc), wu);
-    ldv(C.kv(WF(s), k), sv);
-    ldv(C.kv(WF(l), k), lv);
-    const T rdt = C.kv(WF(rdt), k)[0];
-    T dx[9], dtt, du[NU], dlt[8], dls;
-    for (int i = 0; i < 6; ++i) dx[i] = -(T(1) / C.prm->Wx[i]) * (rdx[i] + ex[i]);
-    {
-        T Lk[36], z1[8], iden, dsl;
-        tr_factor(C, sv, lv, Lk, z1, iden, dsl);
-        const T vL[3] = {-(rdx[6] + ex[6]), -(rdx[7] + ex[7]), -(rdx[8] + ex[8])};
-        tr_local(C, Lk, z1, dsl, iden, vL, -rdt, rh, dx + 6, dtt, dlt, dls);
-    }
-    {
-        T au[NU];
-        phi_solve_u(C, kc, eu, au);
-        for (int i = 0; i < NU; ++i) du[i] = hu ? -wu[i] - au[i] : T(0);
-    }
-    constexpr int ld = KPC;
-    const T amax = dz_rows<T, ROBOT>(C, k, dx, dtt, du, eu, dlt, dls, rh, sv, lv, ld, C.stage + kc,
-                                     C.ws + WF(rdu) * KPC + kc, C.ws + WF(rdi) * KPC + k,
-                                     C.ws + (corr ? WF(ds) : WF(dsa)) * KPC + k,
-                                     C.ws + (corr ? WF(dl) : WF(dla)) * KPC + k, mus);
-    stv(C.kv(WF(dx), k), dx);
-    C.kv(WF(dt), k)[0] = dtt;
-    if (hu) stv(C.kv(WF(du), k), du);
-    return amax;
+    const int kc = k < C.N ? k : 0;   // k = N: no controls or contacts
+    T *ws = C.ws;
+    return dz_knot<T, ROBOT>(C, k, mus, C.stage + kc, ws + WF(rh) * KPC + k, ws + WF(rdx) * KPC + k,
+                             ws + WF(rdt) * KPC + k, ws + WF(wu) * KPC + kc, ws + WF(s) * KPC + k,
+                             ws + WF(l) * KPC + k, ws + WF(rdi) * KPC + k, ws + WF(rdu) * KPC + kc,
+                             ws + WF(facu) * KPC + kc, ws + WF(dx) * KPC + k, ws + WF(dt) * KPC + k,
+                             ws + WF(du) * KPC + k, ws + (corr ? WF(ds) : WF(dsa)) * KPC + k,
+                             ws + (corr ? WF(dl) : WF(dla)) * KPC + k);
 }
 
 // z, nu, s, lambda += a * direction (dnu from the LDS vector)
