@@ -46,6 +46,47 @@ __device__ __forceinline__ void wmm(T *Cm, const T *Am, const T *Bm, int lane, c
     wave_sync();
 }
 
+// fp64: the same product on the matrix cores (v_mfma_f64_16x16x4_f64, M, N <= 16): one LDS read
+// per operand per lane and 4-wide k block instead of 2K reads per output.  Lane maps
+// (cdna_hip_programming.md, f64): A lane l = A[l & 15][4 kb + (l >> 4)], B lane l =
+// B[4 kb + (l >> 4)][l & 15], C/D lane l register r = C[(l >> 4) + 4 r][l & 15].
+typedef double lin_v4d __attribute__((ext_vector_type(4)));
+template <int M, int N, int K, bool TA, bool TB>
+__device__ __forceinline__ void wmm(double *Cm, const double *Am, const double *Bm, int lane,
+                                    const double *Cadd = nullptr, double alpha = 1.0) {
+    static_assert(M <= 16 && N <= 16, "one 16x16 tile");
+    const int r16 = lane & 15, q4 = lane >> 4;
+    lin_v4d acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kb = 0; kb < (K + 3) / 4; ++kb) {
+        const int kk = 4 * kb + q4;
+        const bool ka = kk < K;
+        const int kc = ka ? kk : K - 1;
+        const int ia = r16 < M ? r16 : M - 1, jb = r16 < N ? r16 : N - 1;
+        const double a = TA ? Am[kc * M + ia] : Am[ia * K + kc];
+        const double bb = TB ? Bm[jb * K + kc] : Bm[kc * N + jb];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64((ka && r16 < M) ? a : 0.0, (ka && r16 < N) ? bb : 0.0, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = q4 + 4 * r, j = r16;
+        if (i < M && j < N) {
+            double v = alpha * acc[r];
+            if (Cadd) v += Cadd[i * N + j];
+            Cm[i * N + j] = v;
+        }
+    }
+    wave_sync();
+}
+
+// entry (r, j) of the cross-product matrix [v]x by selects (a runtime-indexed local array would
+// live in scratch memory)
+template <typename T, typename V> __device__ __forceinline__ T skew_at(const V &v, int r, int j) {
+    const int idx = 3 - r - j;
+    const T e = idx == 0 ? T(v[0]) : (idx == 1 ? T(v[1]) : T(v[2]));
+    return r == j ? T(0) : ((j - r + 3) % 3 == 1 ? -e : e);
+}
+
 template <typename T> __device__ __forceinline__ T lin_rcp(T p) {
     T r;
     if constexpr (sizeof(T) == 8) r = __builtin_amdgcn_rcp(p); else r = __builtin_amdgcn_rcpf(p);
@@ -153,8 +194,7 @@ __device__ void linearize_knot(const DevBuf<T> &d, const DevParams<T> &prm, int 
             T w[3] = {0, 0, 0};
             for (int c = 0; c < NC; ++c)
                 for (int q = 0; q < 3; ++q) w[q] += s.a[c] * s.u[NUPC * c + FO + q];
-            const T sk[9] = {0, -w[2], w[1], w[2], 0, -w[0], -w[1], w[0], 0};
-            v = dt * sk[r * 3 + j];
+            v = dt * skew_at<T>(w, r, j);
         }
         s.A[e] = v;
         d.A[kn * 81 + e] = v;
@@ -174,16 +214,14 @@ __device__ void linearize_knot(const DevBuf<T> &d, const DevParams<T> &prm, int 
             const int fq = q - FO;
             if (i >= 3 && i < 6) v = (i - 3 == fq) ? ac : T(0);
             if (i >= 6) {
-                const T sk[9] = {0, -lev[2], lev[1], lev[2], 0, -lev[0], -lev[1], lev[0], 0};
-                v = ac * sk[(i - 6) * 3 + fq];
+                v = ac * skew_at<T>(lev, i - 6, fq);
             }
         } else if (ROBOT == 1 && i >= 6) {
             const T *Rc = &s.R[9 * c];
             const int r = i - 6;
             if (q < 2) {   // -[f]x R[:, q]
-                const T sk[9] = {0, -f[2], f[1], f[2], 0, -f[0], -f[1], f[0], 0};
                 T acc = 0;
-                for (int z = 0; z < 3; ++z) acc += sk[r * 3 + z] * Rc[z * 3 + q];
+                for (int z = 0; z < 3; ++z) acc += skew_at<T>(f, r, z) * Rc[z * 3 + q];
                 v = -ac * acc;
             } else {       // tau: R[:, 2]
                 v = ac * Rc[r * 3 + 2];
@@ -197,8 +235,7 @@ __device__ void linearize_knot(const DevBuf<T> &d, const DevParams<T> &prm, int 
         T v = T(0);
         if (i >= 6) {   // -dt a [f]x
             const T *f = &s.u[NUPC * c + FO];
-            const T sk[9] = {0, -f[2], f[1], f[2], 0, -f[0], -f[1], f[0], 0};
-            v = -dt * s.a[c] * sk[(i - 6) * 3 + q];
+            v = -dt * s.a[c] * skew_at<T>(f, i - 6, q);
         }
         s.Cm[e] = v;
         d.C[kn * 9 * NW + e] = v;
