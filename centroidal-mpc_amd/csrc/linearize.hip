@@ -339,6 +339,13 @@ __global__ void __launch_bounds__(256, 4) k_linearize(DevBuf<T> d, int only_acti
     issue(0);
     land(0);
     wave_sync();
+    // fp64: Sigma stays in the matrix-core accumulator layout for the whole scan (C/D lane l,
+    // register r = Sigma[(l >> 4) + 4 r][l & 15]).  Y = Sigma Acl' takes Sigma as its A operand
+    // straight from those registers (Sigma is symmetric, so register kb holds A[l & 15][4 kb +
+    // (l >> 4)]); Sigma' = Acl Y + Qw takes Y as its B operand the same way (it sums over Y's
+    // row index).  Per step only Acl and Qw are read from LDS.
+    [[maybe_unused]] lin_v4d Sreg = {0.0, 0.0, 0.0, 0.0};
+    const int r16 = lane & 15, q4 = lane >> 4;
     for (int c = 0; c * KS < N; ++c) {
         issue(c + 1);
         const T *cb = buf + (c & 1) * CH;
@@ -346,6 +353,33 @@ __global__ void __launch_bounds__(256, 4) k_linearize(DevBuf<T> d, int only_acti
             const int k = c * KS + q;
             if (k >= N) break;
             const T *Ac = cb + q * 81, *Q = cb + (KS + q) * 81;
+            if constexpr (sizeof(T) == 8) {
+                double av[3];   // Acl[l & 15][4 kb + (l >> 4)] (zero outside 9 x 9)
+#pragma unroll
+                for (int kb = 0; kb < 3; ++kb) {
+                    const int m = 4 * kb + q4;
+                    av[kb] = (r16 < 9 && m < 9) ? Ac[(r16 < 9 ? r16 : 0) * 9 + (m < 9 ? m : 0)] : 0.0;
+                }
+                lin_v4d qw;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = q4 + 4 * r;
+                    qw[r] = (i < 9 && r16 < 9) ? Q[(i < 9 ? i : 0) * 9 + (r16 < 9 ? r16 : 0)] : 0.0;
+                }
+                lin_v4d Y = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int kb = 0; kb < 3; ++kb) Y = __builtin_amdgcn_mfma_f64_16x16x4f64(Sreg[kb], av[kb], Y, 0, 0, 0);
+                Sreg = qw;
+#pragma unroll
+                for (int kb = 0; kb < 3; ++kb) Sreg = __builtin_amdgcn_mfma_f64_16x16x4f64(av[kb], Y[kb], Sreg, 0, 0, 0);
+                T *so = d.Sig + ((size_t)b * (N + 1) + k + 1) * 81;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = q4 + 4 * r;
+                    if (i < 9 && r16 < 9) so[i * 9 + r16] = Sreg[r];
+                }
+                continue;
+            }
             for (int e = lane; e < 81; e += WAVE) {     // Tm = Acl S
                 const int i = e / 9, j = e % 9;
                 T a[9], sv[9];
