@@ -829,6 +829,8 @@ __device__ __forceinline__ void tw_step(const LdsT<T> *Dn, const LdsT<T> *Op, co
 #else
 #define SUBSTAMP(i) do { } while (0)
 #endif
+    // lanes past element 80 hold a clamped copy of element 80 and compute bit-identical values,
+    // so their LDS stores (the same value to the same slot) need no mask; global stores keep it
     const int l = threadIdx.x & (L - 1);
     int e[NE], ii[NE], cc[NE];
     bool ok[NE];
@@ -846,7 +848,7 @@ __device__ __forceinline__ void tw_step(const LdsT<T> *Dn, const LdsT<T> *Op, co
     // original diagonal of S_jj (pivot floor): entries 0, 10, ..., 80
 #pragma unroll
     for (int q = 0; q < NE; ++q)
-        if (ok[q] && e[q] % 10 == 0) Dd[e[q] / 10] = a[q];
+        if (e[q] % 10 == 0) Dd[e[q] / 10] = a[q];
     // 9-term dot products with every LDS operand read before the first multiply
     auto dot = [&](auto fa, auto fb) -> T {
         T u[9], v[9];
@@ -862,8 +864,7 @@ __device__ __forceinline__ void tw_step(const LdsT<T> *Dn, const LdsT<T> *Op, co
         for (int q = 0; q < NE; ++q)
             x[q] = dot([&](int m) { return Op[m * 9 + ii[q]]; }, [&](int m) { return Ip[m * 9 + cc[q]]; });
 #pragma unroll
-        for (int q = 0; q < NE; ++q)
-            if (ok[q]) Xb[e[q]] = x[q];
+        for (int q = 0; q < NE; ++q) Xb[e[q]] = x[q];
         wave_sync();
         if (vb && l < 9) rv -= dot9(Xb + l * 9, vb + jx * 9);
 #pragma unroll
@@ -876,8 +877,7 @@ __device__ __forceinline__ void tw_step(const LdsT<T> *Dn, const LdsT<T> *Op, co
         for (int q = 0; q < NE; ++q)
             y[q] = dot([&](int m) { return Oq[ii[q] * 9 + m]; }, [&](int m) { return Iq[m * 9 + cc[q]]; });
 #pragma unroll
-        for (int q = 0; q < NE; ++q)
-            if (ok[q]) Xb[e[q]] = y[q];
+        for (int q = 0; q < NE; ++q) Xb[e[q]] = y[q];
         wave_sync();
         if (vb && l < 9) rv -= dot9(Xb + l * 9, vb + jy * 9);
 #pragma unroll
@@ -887,8 +887,8 @@ __device__ __forceinline__ void tw_step(const LdsT<T> *Dn, const LdsT<T> *Op, co
     }
 #pragma unroll
     for (int q = 0; q < NE; ++q) {
-        if (!ok[q]) continue;
         A[e[q]] = a[q];
+        if (!ok[q]) continue;
         if (Op) Xout[e[q]] = x[q];
         if (Oq) Yout[e[q]] = y[q];
     }
@@ -912,21 +912,21 @@ __device__ __forceinline__ void tw_step(const LdsT<T> *Dn, const LdsT<T> *Op, co
         for (int q = 0; q < NE; ++q) {
             const T mi = aic[q] * ip;
             const T gen = fma(-mi, acj[q], a[q]), row = acj[q] * ip, col = -mi;
-            a[q] = ii[q] == c ? (cc[q] == c ? ip : row) : (cc[q] == c ? col : gen);
+            // selects, not branches (the compiler otherwise splits the lanes into divergent paths)
+            const bool ic = __builtin_unpredictable(ii[q] == c), jc = __builtin_unpredictable(cc[q] == c);
+            a[q] = ic ? (jc ? ip : row) : (jc ? col : gen);
         }
         wave_sync();
 #pragma unroll
-        for (int q = 0; q < NE; ++q)
-            if (ok[q]) A[e[q]] = a[q];
+        for (int q = 0; q < NE; ++q) A[e[q]] = a[q];
         wave_sync();
         ip = ipn;
     }
     SUBSTAMP(1);
 #pragma unroll
     for (int q = 0; q < NE; ++q) {
-        if (!ok[q]) continue;
         P[e[q]] = a[q];
-        Iout[e[q]] = a[q];
+        if (ok[q]) Iout[e[q]] = a[q];
     }
     if (vb) {
         if (Op && Oq) {   // meeting block: x_m = I_m (b_m - X_m y_{m-1} - Y_m y_{m+1})
@@ -972,8 +972,7 @@ __device__ void tw_factor_ends(T *Sd, T *So, int NB, int m, LdsT<T> *sh, LdsT<T>
 #pragma unroll
         for (int q = 0; q < NE; ++q) v[q] = D0[e[q]];
 #pragma unroll
-        for (int q = 0; q < NE; ++q)
-            if (ok[q]) Dn[e[q]] = v[q];
+        for (int q = 0; q < NE; ++q) Dn[e[q]] = v[q];
     }
     wave_sync();
     for (int s = 0, j = j0; s < m; ++s, j += dj) {
@@ -996,8 +995,7 @@ __device__ void tw_factor_ends(T *Sd, T *So, int NB, int m, LdsT<T> *sh, LdsT<T>
         const unsigned long long tl = __builtin_amdgcn_s_memtime();
 #endif
 #pragma unroll
-        for (int q = 0; q < NE; ++q)
-            if (ok[q]) { Ob[et[q]] = pv[q]; Dn[e[q]] = nv[q]; }
+        for (int q = 0; q < NE; ++q) { Ob[et[q]] = pv[q]; Dn[e[q]] = nv[q]; }   // clamped lanes: same values
         wave_sync();
 #ifdef CMPC_STAMPS
         if (subp) sub[3] += __builtin_amdgcn_s_memtime() - tl;
@@ -1055,8 +1053,7 @@ template <typename T, int K> struct ChunkStream {
 #pragma unroll
         for (int q = 0; q < K; ++q)
 #pragma unroll
-            for (int g = 0; g < 3; ++g)
-                if (l + 32 * g < 81) b[q * RSLOT + l + 32 * g] = r[q][g];
+            for (int g = 0; g < 3; ++g) b[q * RSLOT + (l + 32 * g < 81 ? l + 32 * g : 80)] = r[q][g];   // clamped: same value
     }
     __device__ __forceinline__ const LdsT<T> *blk(int i) const {
         return buf + ((i / K) & 1) * K * RSLOT + (i % K) * RSLOT;

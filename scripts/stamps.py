@@ -18,6 +18,12 @@ names = ['residual', 'factor+w_pred', 'sblock+rhs_pred', 'seq_factor+elim', 'w_c
 its = s.qp_iterations_total() / B
 tot = st[:, :9].sum(axis=1).mean()
 print('B', B, 'N', N, 'qp_ms', t['qp_ms'], 'ipm iters', its, 'cycles/problem %.3g' % tot)
+_, _, _, itv = s.qp_solution(with_y=False)
+print('  ipm iterations of the last solve: mean %.2f  p50 %d  p90 %d  p99 %d  max %d' % (
+    itv.mean(), np.percentile(itv, 50), np.percentile(itv, 90), np.percentile(itv, 99), itv.max()))
+tq = st[:, :9].sum(axis=1)
+print('  per-problem QP cycles (warm-up + timed): p50 %.3g  p90 %.3g  max %.3g' % (
+    np.percentile(tq, 50), np.percentile(tq, 90), tq.max()))
 for i, n in enumerate(names):
     print('  %-11s %5.1f%%  %.3g cycles/IPM-iter' % (n, 100 * st[:, i].mean() / tot, st[:, i].mean() / its))
 # tw_factor_ends sub-steps (top wave; accumulated over the warm-up and the timed iteration)
