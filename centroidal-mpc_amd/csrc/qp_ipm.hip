@@ -35,9 +35,9 @@
 namespace cmpc {
 
 constexpr int NT = IPM_NT;   // one wave: a half-wave per end of the Schur sweeps; knots k, k + 64, ...
-// Stored parts of the Phi factors (phase_factor -> phase_sblock, phi_solve_u); the rest (the
-// trust-region Cholesky factor, each contact's G W^-1 and Kinv) is recomputed in registers by the
-// phases that use it (tr_factor, fric_factor), which costs less than its HBM round trip.
+// Stored parts of the Phi factors (phase_factor -> phase_sblock); the w and direction phases
+// recompute everything they need (the trust-region Cholesky factor, each contact's G W^-1, Kinv,
+// F and W'^-1: tr_factor, fric_factor, fric_F, contact_wd), which costs less than its HBM round trip.
 constexpr int FU = 12, FU_F = 0, FU_WI = 6;   // per contact: F = [Phi_u^-1] force block, packed 6 | 1 / W' diagonal 6
 constexpr int FX = 6, FX_ML = 0;               // per knot: M_LL = [Phi^-1]_LL packed 6
 
@@ -361,6 +361,41 @@ __device__ __forceinline__ void fric_factor(const T (&G)[12], const T (&wi)[3], 
     for (int q = 0; q < 10; ++q) Ki[q] = (q == 0 || q == 2 || q == 5 || q == 9) ? fma(Ki[q], on, off) : Ki[q] * on;
 }
 
+// force block of Phi_u^-1 for one contact: F = W^-1 - Gw' Kinv Gw (packed 00,10,11,20,21,22);
+// inactive contacts (Gw = 0): F = W^-1
+template <typename T>
+__device__ __forceinline__ void fric_F(const T (&Gw)[4][3], const T (&Ki)[10], const T (&wi)[3], T (&F)[6]) {
+    int p = 0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j) {
+            T acc = (i == j) ? wi[i] : T(0);
+            for (int r = 0; r < 4; ++r)
+                for (int q = 0; q < 4; ++q) acc -= Gw[r][i] * Ki[p4(r, q)] * Gw[q][j];
+            F[p++] = acc;
+        }
+}
+
+// inverse diagonal of W' for one contact's controls: 1 / W, except TALOS's CoP coordinates of an
+// active contact, whose two bound rows fold in as D-form (1 / (W + D_lo + D_hi)); s, lm indexed by row
+template <typename T, int ROBOT, typename SA>
+__device__ __forceinline__ void contact_wd(const Ctx<T, ROBOT> &C, int c, bool act, const SA &s, const SA &lm,
+                                           T (&wd)[Robot<ROBOT>::NUPC]) {
+    constexpr int NUPC = Robot<ROBOT>::NUPC;
+    const T *Wc = C.prm->Wu + NUPC * c;
+#pragma unroll
+    for (int q = 0; q < NUPC; ++q) wd[q] = T(1) / Wc[q];
+    if (ROBOT == 1) {
+#pragma unroll
+        for (int dd = 0; dd < 2; ++dd) {
+            const int r0 = Rows<ROBOT>::CP + 4 * c + 2 * dd;
+            const T v = T(1) / (Wc[dd] + C.Dform(lm[r0], s[r0]) + C.Dform(lm[r0 + 1], s[r0 + 1]));
+            wd[dd] = act ? v : wd[dd];
+        }
+    }
+}
+
 // ------------------------------------------------------------------ phases
 // (1) residuals of knot k; returns norm contributions
 template <typename T, int ROBOT> struct Norms { T prim, dual, comp, mu, sp, sd, lmax, cnt; };
@@ -589,30 +624,10 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_factor(const C
         }
         T Gw[4][3], Ki[10];
         fric_factor(Gr[c], wi, s + R_::FR + 4 * c, lm + R_::FR + 4 * c, true, Gw, Ki);
-        // F = W^-1 - Gw' Kinv Gw  (stored for phi_solve_u and phase_sblock)
-        int p = 0;
-        for (int i = 0; i < 3; ++i)
-            for (int j = 0; j <= i; ++j) {
-                T acc = (i == j) ? wi[i] : T(0);
-                for (int r = 0; r < 4; ++r)
-                    for (int q = 0; q < 4; ++q) acc -= Gw[r][i] * Ki[p4(r, q)] * Gw[q][j];
-                fu[FU_F + p++] = acc;
-            }
-    }
-}
-
-// Phi_u^-1 vu for the control blocks of knot k < N (friction rows in push-through form)
-template <typename T, int ROBOT> __device__ void phi_solve_u(const Ctx<T, ROBOT> &C, int k, const T *vu, T *ou) {
-    constexpr int NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
-    for (int c = 0; c < NC; ++c) {
-        const SV<T> fu = C.kv(WF(facu), k) + c * FU;
-        const T *vc = vu + NUPC * c;
-        T *oc = ou + NUPC * c;
-        for (int q = 0; q < NUPC; ++q) oc[q] = fu[FU_WI + q] * vc[q];
+        // F = W^-1 - Gw' Kinv Gw  (stored for phase_sblock)
         T F[6];
-        ldv(fu + FU_F, F);
-        for (int i = 0; i < 3; ++i)
-            oc[FO + i] = sym3(F, i, 0) * vc[FO] + sym3(F, i, 1) * vc[FO + 1] + sym3(F, i, 2) * vc[FO + 2];
+        fric_F(Gw, Ki, wi, F);
+        for (int q = 0; q < 6; ++q) fu[FU_F + q] = F[q];
     }
 }
 
@@ -1236,17 +1251,23 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_w(const Ctx<T,
                     vu[NUPC * c + dd] += C.Dform(lv[r0], sv[r0]) * rh[r0] - C.Dform(lv[r0 + 1], sv[r0 + 1]) * rh[r0 + 1];
                 }
         }
-        phi_solve_u(C, k, vu, ou);
         const auto st = C.st(k);
         const unsigned msk = C.cmask(k);
 #pragma unroll
-        for (int c = 0; c < NC; ++c) {
+        for (int c = 0; c < NC; ++c) {   // Phi_u^-1 (vu + G' D rhat) contact by contact
+            const bool act = (msk >> c) & 1u;
             T G[12];
             ldv(st + (S::CON + S::CS * c + S::G), G);
             const T *Wc = P.Wu + NUPC * c;
             const T wi[3] = {T(1) / Wc[FO], T(1) / Wc[FO + 1], T(1) / Wc[FO + 2]};
-            T Gw[4][3], Ki[10];
-            fric_factor(G, wi, sv + R_::FR + 4 * c, lv + R_::FR + 4 * c, (msk >> c) & 1u, Gw, Ki);
+            T Gw[4][3], Ki[10], F[6], wd[NUPC];
+            fric_factor(G, wi, sv + R_::FR + 4 * c, lv + R_::FR + 4 * c, act, Gw, Ki);
+            fric_F(Gw, Ki, wi, F);
+            contact_wd(C, c, act, sv, lv, wd);
+            const T *vc = vu + NUPC * c;
+            for (int q = 0; q < NUPC; ++q) ou[NUPC * c + q] = wd[q] * vc[q];
+            for (int i = 0; i < 3; ++i)
+                ou[NUPC * c + FO + i] = sym3(F, i, 0) * vc[FO] + sym3(F, i, 1) * vc[FO + 1] + sym3(F, i, 2) * vc[FO + 2];
             T kr[4];
             for (int r = 0; r < 4; ++r) {
                 T acc = T(0);
@@ -1302,7 +1323,7 @@ template <typename T, int ROBOT>
 __device__ __forceinline__ T dz_knot(const Ctx<T, ROBOT> &C, int k, T (&mus)[3], const T *__restrict__ stp,
                                      const T *__restrict__ rhp, const T *__restrict__ rdxp, const T *__restrict__ rdtp,
                                      const T *__restrict__ wup, const T *__restrict__ ss, const T *__restrict__ ls,
-                                     const T *__restrict__ rdip, const T *__restrict__ rdup, const T *__restrict__ fup,
+                                     const T *__restrict__ rdip, const T *__restrict__ rdup,
                                      T *__restrict__ dxo, T *__restrict__ dto, T *__restrict__ duo, T *__restrict__ ds,
                                      T *__restrict__ dl) {
     using S = Stage<ROBOT>;
@@ -1369,10 +1390,22 @@ __device__ __forceinline__ T dz_knot(const Ctx<T, ROBOT> &C, int k, T (&mus)[3],
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         const bool pr = hu && ((msk >> c) & 1u);
-        const T *fu = fup + c * FU * ld;
-        T F[6], wd[NUPC], au[NUPC], du[NUPC];
-        for (int q = 0; q < 6; ++q) F[q] = fu[(FU_F + q) * ld];
-        for (int q = 0; q < NUPC; ++q) wd[q] = fu[(FU_WI + q) * ld];
+        const auto cs = st + (S::CON + S::CS * c);
+        T G[12], s4[4], l4[4], rh4[4], ri4[4], vf[3];
+        for (int e = 0; e < 12; ++e) G[e] = cs[S::G + e];
+        for (int r = 0; r < 4; ++r) {
+            const int row = R_::FR + 4 * c + r;
+            s4[r] = ss[row * ld]; l4[r] = ls[row * ld]; rh4[r] = rhp[row * ld]; ri4[r] = rdip[row * ld];
+        }
+        const T *Wc = C.prm->Wu + NUPC * c;
+        const T wi[3] = {T(1) / Wc[FO], T(1) / Wc[FO + 1], T(1) / Wc[FO + 2]};
+        T Gw[4][3], Ki[10], F[6], wd[NUPC], au[NUPC], du[NUPC];
+        fric_factor(G, wi, s4, l4, pr, Gw, Ki);
+        fric_F(Gw, Ki, wi, F);
+        {
+            const SV<const T> sS{ss}, lS{ls};
+            contact_wd(C, c, pr, sS, lS, wd);
+        }
         const T *ec = eu + NUPC * c;
         for (int q = 0; q < NUPC; ++q) au[q] = wd[q] * ec[q];
         for (int i = 0; i < 3; ++i)
@@ -1383,18 +1416,7 @@ __device__ __forceinline__ T dz_knot(const Ctx<T, ROBOT> &C, int k, T (&mus)[3],
         for (int q = 0; q < NUPC; ++q) du[q] = (-wup[(NUPC * c + q) * ld] - au[q]) * hf;
         if (hu)
             for (int q = 0; q < NUPC; ++q) duo[(NUPC * c + q) * ld] = du[q];
-        const auto cs = st + (S::CON + S::CS * c);
-        T G[12], s4[4], l4[4], rh4[4], ri4[4], vf[3];
-        for (int e = 0; e < 12; ++e) G[e] = cs[S::G + e];
-        for (int r = 0; r < 4; ++r) {
-            const int row = R_::FR + 4 * c + r;
-            s4[r] = ss[row * ld]; l4[r] = ls[row * ld]; rh4[r] = rhp[row * ld]; ri4[r] = rdip[row * ld];
-        }
         for (int i = 0; i < 3; ++i) vf[i] = -(rdup[(NUPC * c + FO + i) * ld] + ec[FO + i]) * hf;
-        const T *Wc = C.prm->Wu + NUPC * c;
-        const T wi[3] = {T(1) / Wc[FO], T(1) / Wc[FO + 1], T(1) / Wc[FO + 2]};
-        T Gw[4][3], Ki[10];
-        fric_factor(G, wi, s4, l4, pr, Gw, Ki);
         T z[4];
         for (int r = 0; r < 4; ++r) z[r] = Gw[r][0] * vf[0] + Gw[r][1] * vf[1] + Gw[r][2] * vf[2] + rh4[r];
 #pragma unroll
@@ -1424,7 +1446,7 @@ __device__ PHASE_ATTR T phase_dz(const Ctx<T, ROBOT> &C, int k, int corr, T (&mu
     return dz_knot<T, ROBOT>(C, k, mus, C.stage + kc, ws + WF(rh) * KPC + k, ws + WF(rdx) * KPC + k,
                              ws + WF(rdt) * KPC + k, ws + WF(wu) * KPC + kc, ws + WF(s) * KPC + k,
                              ws + WF(l) * KPC + k, ws + WF(rdi) * KPC + k, ws + WF(rdu) * KPC + kc,
-                             ws + WF(facu) * KPC + kc, ws + WF(dx) * KPC + k, ws + WF(dt) * KPC + k,
+                             ws + WF(dx) * KPC + k, ws + WF(dt) * KPC + k,
                              ws + WF(du) * KPC + k, ws + (corr ? WF(ds) : WF(dsa)) * KPC + k,
                              ws + (corr ? WF(dl) : WF(dla)) * KPC + k);
 }
