@@ -1195,12 +1195,11 @@ __device__ __forceinline__ void rhat_rows(const Ctx<T, ROBOT> &C, int k, int cor
     ldv(C.kv(WF(rdi), k), rd);
 #pragma unroll
     for (int r = 0; r < NI; ++r) cc[r] = T(0);
-    if (corr) {   // corrector: + ds_aff dlambda_aff - sigma mu
-        T a[NI], b[NI];
+    if (corr) {   // corrector: + ds_aff dlambda_aff - sigma mu (the product, stored by the predictor)
+        T a[NI];
         ldv(C.kv(WF(dsa), k), a);
-        ldv(C.kv(WF(dla), k), b);
 #pragma unroll
-        for (int r = 0; r < NI; ++r) cc[r] = a[r] * b[r] - sigma_mu;
+        for (int r = 0; r < NI; ++r) cc[r] = a[r] - sigma_mu;
     }
 #pragma unroll
     for (int r = 0; r < NI; ++r) {
@@ -1320,7 +1319,7 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_rhs(const Ctx<
 // is never held in registers whole.  Inactive contacts: G = Gw = 0, Kinv = I, rhat = 0 -> zero
 // steps.
 template <typename T, int ROBOT>
-__device__ __forceinline__ T dz_knot(const Ctx<T, ROBOT> &C, int k, T (&mus)[3], const T *__restrict__ stp,
+__device__ __forceinline__ T dz_knot(const Ctx<T, ROBOT> &C, int k, T (&mus)[3], bool prod, const T *__restrict__ stp,
                                      const T *__restrict__ rhp, const T *__restrict__ rdxp, const T *__restrict__ rdtp,
                                      const T *__restrict__ wup, const T *__restrict__ ss, const T *__restrict__ ls,
                                      const T *__restrict__ rdip, const T *__restrict__ rdup,
@@ -1345,9 +1344,11 @@ __device__ __forceinline__ T dz_knot(const Ctx<T, ROBOT> &C, int k, T (&mus)[3],
     for (int i = 0; i < 9; ++i)
         ex[i] = (k == 0 ? dk[i] : -dk[i]) + (hu ? a[i] : T(0)) + (k == N ? d1[i] : T(0));
     T amax = T(1);
+    // stores: corrector ds, dl; predictor ds_aff dl_aff in the ds field (the corrector's r_hat
+    // term) or, in the initialization step (whose full step is the affine one), ds_aff itself
     auto emit = [&](int r, bool pr, T g, T dlr, T sr, T lr, T rdir) {
         const T dsr = pr ? -rdir - g : T(0);
-        ds[r * ld] = dsr;
+        ds[r * ld] = prod ? dsr * dlr : dsr;
         dl[r * ld] = dlr;
         // sum_r (s + a ds)(lambda + a dl) = mus0 + a mus1 + a^2 mus2 (absent rows: lambda = ds = dl = 0)
         mus[0] = fma(sr, lr, mus[0]);
@@ -1440,10 +1441,10 @@ __device__ __forceinline__ T dz_knot(const Ctx<T, ROBOT> &C, int k, T (&mus)[3],
 }
 
 template <typename T, int ROBOT>
-__device__ PHASE_ATTR T phase_dz(const Ctx<T, ROBOT> &C, int k, int corr, T (&mus)[3]) {
+__device__ PHASE_ATTR T phase_dz(const Ctx<T, ROBOT> &C, int k, int corr, bool init, T (&mus)[3]) {
     const int kc = k < C.N ? k : 0;   // k = N: no controls or contacts
     T *ws = C.ws;
-    return dz_knot<T, ROBOT>(C, k, mus, C.stage + kc, ws + WF(rh) * KPC + k, ws + WF(rdx) * KPC + k,
+    return dz_knot<T, ROBOT>(C, k, mus, !corr && !init, C.stage + kc, ws + WF(rh) * KPC + k, ws + WF(rdx) * KPC + k,
                              ws + WF(rdt) * KPC + k, ws + WF(wu) * KPC + kc, ws + WF(s) * KPC + k,
                              ws + WF(l) * KPC + k, ws + WF(rdi) * KPC + k, ws + WF(rdu) * KPC + kc,
                              ws + WF(dx) * KPC + k, ws + WF(dt) * KPC + k,
@@ -1650,7 +1651,7 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
             __syncthreads();
             STAMP(6);
             T am[1] = {T(1)}, mus[3] = {T(0), T(0), T(0)};
-            for (int k = tid; k < K1; k += NT) am[0] = fmin(am[0], phase_dz<T, ROBOT>(C, k, corr, mus));
+            for (int k = tid; k < K1; k += NT) am[0] = fmin(am[0], phase_dz<T, ROBOT>(C, k, corr, init, mus));
             block_reduce<T, NT, 1, 2>(am, red);
             STAMP(7);
             alpha = am[0];
