@@ -225,7 +225,7 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
         break;
     }
     case 3:
-        hipLaunchKernelGGL((k_accept<T, R>), dim3(B), dim3(256), 0, h->stream, d, only_active ? 0 : 1);
+        hipLaunchKernelGGL((k_accept<T, R>), dim3(B), dim3(64), 0, h->stream, d, only_active ? 0 : 1);   // ACC_NT
         break;
     }
     HIPCHK(hipGetLastError());

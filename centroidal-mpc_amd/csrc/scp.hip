@@ -15,27 +15,77 @@ namespace cmpc {
 
 enum { DEC_NONE = 0, DEC_ACCEPT = 1, DEC_REJECT_RHO = 2, DEC_REJECT_TR = 3, DEC_QP_FAILED = -1 };
 
-template <int n> __device__ double jacobi_lambda_max(double (&a)[n][n]) {
+// Largest eigenvalue of the symmetric n x n matrix a (row-major, in LDS: rotations index it at run
+// time, which would put a private array in scratch memory), cyclic Jacobi on one thread.
+template <int n> __device__ double jacobi_lambda_max(double *a_) {
+    auto a = [&](int i, int j) -> double & { return a_[i * n + j]; };
     for (int sweep = 0; sweep < 40; ++sweep) {
         double off = 0.0, tot = 0.0;
         for (int i = 0; i < n; ++i)
+            for (int j = 0; j < n; ++j) {
+                tot += a(i, j) * a(i, j);
+                if (i != j) off += a(i, j) * a(i, j);
+            }
+        if (off <= 1e-30 * tot || off == 0.0) break;
+        for (int p = 0; p < n - 1; ++p)
+            for (int q = p + 1; q < n; ++q) {
+                const double apq = a(p, q);
+                if (apq == 0.0) continue;
+                const double theta = (a(q, q) - a(p, p)) / (2.0 * apq);
+                const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+                for (int k = 0; k < n; ++k) {
+                    const double akp = a(k, p), akq = a(k, q);
+                    a(k, p) = c * akp - s * akq;
+                    a(k, q) = s * akp + c * akq;
+                }
+                for (int k = 0; k < n; ++k) {
+                    const double apk = a(p, k), aqk = a(q, k);
+                    a(p, k) = c * apk - s * aqk;
+                    a(q, k) = s * apk + c * aqk;
+                }
+            }
+    }
+    double m = a(0, 0);
+    for (int i = 1; i < n; ++i) m = fmax(m, a(i, i));
+    return m;
+}
+
+// The same in registers for small n: every rotation loop unrolled so all indices are constants
+// (the matrix lives in VGPRs; LDS or scratch put a ~100-cycle access in every dependent step)
+template <int n> __device__ double jacobi_lambda_max_reg(const double *g) {
+    double a[n][n];
+#pragma unroll
+    for (int i = 0; i < n; ++i)
+#pragma unroll
+        for (int j = 0; j < n; ++j) a[i][j] = g[i * n + j];
+    for (int sweep = 0; sweep < 40; ++sweep) {
+        double off = 0.0, tot = 0.0;
+#pragma unroll
+        for (int i = 0; i < n; ++i)
+#pragma unroll
             for (int j = 0; j < n; ++j) {
                 tot += a[i][j] * a[i][j];
                 if (i != j) off += a[i][j] * a[i][j];
             }
         if (off <= 1e-30 * tot || off == 0.0) break;
+#pragma unroll
         for (int p = 0; p < n - 1; ++p)
+#pragma unroll
             for (int q = p + 1; q < n; ++q) {
                 const double apq = a[p][q];
-                if (apq == 0.0) continue;
-                const double theta = (a[q][q] - a[p][p]) / (2.0 * apq);
-                const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                // apq == 0: identity rotation (c = 1, s = 0), kept branch-free
+                const double theta = (a[q][q] - a[p][p]) / (2.0 * (apq != 0.0 ? apq : 1.0));
+                const double t0 = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                const double t = apq != 0.0 ? t0 : 0.0;
                 const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+#pragma unroll
                 for (int k = 0; k < n; ++k) {
                     const double akp = a[k][p], akq = a[k][q];
                     a[k][p] = c * akp - s * akq;
                     a[k][q] = s * akp + c * akq;
                 }
+#pragma unroll
                 for (int k = 0; k < n; ++k) {
                     const double apk = a[p][k], aqk = a[q][k];
                     a[p][k] = c * apk - s * aqk;
@@ -44,6 +94,7 @@ template <int n> __device__ double jacobi_lambda_max(double (&a)[n][n]) {
             }
     }
     double m = a[0][0];
+#pragma unroll
     for (int i = 1; i < n; ++i) m = fmax(m, a[i][i]);
     return m;
 }
@@ -54,21 +105,20 @@ template <int n> __device__ double jacobi_lambda_max(double (&a)[n][n]) {
 template <int rows, typename T>
 __device__ double spec_norm(const T *V, const T *W, int cols, double *gram, double *res) {
     const int tid = threadIdx.x;
-    if (tid < rows * rows) {
-        const int i = tid / rows, j = tid % rows;
+    for (int e = tid; e < rows * rows; e += blockDim.x) {
+        const int i = e / rows, j = e % rows;
         double g = 0.0;
         for (int c = 0; c < cols; ++c) {
             const double vi = double(V[(size_t)c * rows + i]) - (W ? double(W[(size_t)c * rows + i]) : 0.0);
             const double vj = double(V[(size_t)c * rows + j]) - (W ? double(W[(size_t)c * rows + j]) : 0.0);
             g += vi * vj;
         }
-        gram[tid] = g;
+        gram[e] = g;
     }
     __syncthreads();
     if (tid == 0) {
-        double a[rows][rows];
-        for (int e = 0; e < rows * rows; ++e) a[e / rows][e % rows] = gram[e];
-        *res = sqrt(fmax(jacobi_lambda_max<rows>(a), 0.0));
+        if constexpr (rows <= 9) *res = sqrt(fmax(jacobi_lambda_max_reg<rows>(gram), 0.0));
+        else *res = sqrt(fmax(jacobi_lambda_max<rows>(gram), 0.0));   // in place (LDS)
     }
     __syncthreads();
     return *res;
@@ -100,8 +150,13 @@ __device__ void step_dyn(const DevParams<T> &prm, const T *x, const T *u, const 
     for (int i = 0; i < 9; ++i) o[i] = x[i] + F[i] * prm.dt;
 }
 
+// one wave per problem: the kernel needs ~250 registers (the 9 x 9 Jacobi lives in them), and
+// with 64-thread workgroups four problems still share a CU (a 256-thread workgroup ran one per CU)
+constexpr int ACC_NT = 64;
+constexpr int ACC_KC = 128, ACC_REC = 9 + 9 + NU;   // knots per rho chunk, LDS record per knot
+
 template <typename T, int ROBOT>
-__global__ void __launch_bounds__(256) k_accept(DevBuf<T> d, int fixed_iters) {
+__global__ void __launch_bounds__(ACC_NT) k_accept(DevBuf<T> d, int fixed_iters) {
     constexpr int NC = Robot<ROBOT>::NC;
     const int b = blockIdx.x;
     if (b >= d.B) return;
@@ -109,6 +164,7 @@ __global__ void __launch_bounds__(256) k_accept(DevBuf<T> d, int fixed_iters) {
     if (!sc.active) return;
     __shared__ T red[2 * 4];
     __shared__ double gram[NU * NU], nres[4];
+    __shared__ T acc_sm[ACC_KC * ACC_REC];
     __shared__ int dec_sh;
     const int tid = threadIdx.x, N = d.N, K1 = N + 1;
     const DevParams<T> &prm = d.params[d.class_id[b]];
@@ -116,26 +172,36 @@ __global__ void __launch_bounds__(256) k_accept(DevBuf<T> d, int fixed_iters) {
     // previous solution = the linearization point (the warm start in reference mode, quirk Q1)
     T *Xb = d.Xlin + (size_t)b * K1 * 9, *Ub = d.Ulin + (size_t)b * N * NU;
     const int qst = d.qp_status[b];
-    // ---- rho (fp of the compute type)
+    // ---- rho (fp of the compute type), in two passes: per knot the nonlinear step and (dx, du)
+    // into LDS, then per (knot, row) the linearized row from that row of A and B (neighbouring
+    // threads read neighbouring rows: coalesced, where a thread per knot strides 648 B)
     T acc[2] = {T(0), T(0)};
-    for (int k = tid; k < N; k += 256) {
-        const size_t kn = (size_t)b * N + k;
-        T nl[9];
-        step_dyn<T, ROBOT>(prm, Xs + (size_t)k * 9, Us + (size_t)k * NU, d.pos + kn * 3 * NC, d.rot + kn * 9 * NC,
-                           d.logic + kn * NC, nl);
-        const T *A = d.A + kn * 81, *Bm = d.Bu + kn * 9 * NU, *f = d.f + kn * 9;
-        T dx[9], du[NU];
-        for (int i = 0; i < 9; ++i) dx[i] = Xs[(size_t)k * 9 + i] - Xb[(size_t)k * 9 + i];
-        for (int i = 0; i < NU; ++i) du[i] = Us[(size_t)k * NU + i] - Ub[(size_t)k * NU + i];
-        for (int i = 0; i < 9; ++i) {
-            T lin = f[i];
-            for (int j = 0; j < 9; ++j) lin = fma(A[i * 9 + j], dx[j], lin);
-            for (int j = 0; j < NU; ++j) lin = fma(Bm[i * NU + j], du[j], lin);
-            if (i >= 6) acc[0] += sq(nl[i] - lin);
+    for (int k0 = 0; k0 < N; k0 += ACC_KC) {
+        const int nk = min(ACC_KC, N - k0);
+        for (int kk = tid; kk < nk; kk += ACC_NT) {
+            const int k = k0 + kk;
+            const size_t kn = (size_t)b * N + k;
+            T *rec = acc_sm + kk * ACC_REC;   // nl (9) | dx (9) | du (NU)
+            step_dyn<T, ROBOT>(prm, Xs + (size_t)k * 9, Us + (size_t)k * NU, d.pos + kn * 3 * NC, d.rot + kn * 9 * NC,
+                               d.logic + kn * NC, rec);
+            for (int i = 0; i < 9; ++i) rec[9 + i] = Xs[(size_t)k * 9 + i] - Xb[(size_t)k * 9 + i];
+            for (int i = 0; i < NU; ++i) rec[18 + i] = Us[(size_t)k * NU + i] - Ub[(size_t)k * NU + i];
+        }
+        __syncthreads();
+        for (int p = tid; p < nk * 9; p += ACC_NT) {
+            const int kk = p / 9, i = p % 9;
+            const size_t kn = (size_t)b * N + k0 + kk;
+            const T *rec = acc_sm + kk * ACC_REC;
+            const T *Ar = d.A + kn * 81 + i * 9, *Br = d.Bu + kn * 9 * NU + i * NU;
+            T lin = d.f[kn * 9 + i];
+            for (int j = 0; j < 9; ++j) lin = fma(Ar[j], rec[9 + j], lin);
+            for (int j = 0; j < NU; ++j) lin = fma(Br[j], rec[18 + j], lin);
+            if (i >= 6) acc[0] += sq(rec[i] - lin);
             acc[1] += lin * lin;
         }
+        __syncthreads();
     }
-    block_reduce<T, 256, 2, 0>(acc, red);
+    block_reduce<T, ACC_NT, 2, 0>(acc, red);
     const double rho = double(acc[0]) / double(acc[1]);
     // ---- spectral norm of X_sol - X_prev (quirk Q6)
     const double tr = spec_norm<9>(Xs, Xb, K1, gram, &nres[0]);
@@ -197,13 +263,13 @@ __global__ void __launch_bounds__(256) k_accept(DevBuf<T> d, int fixed_iters) {
     __syncthreads();
     if (dec_sh != DEC_ACCEPT) return;
     // accepted: keep X, U and this iteration's LQR gains / covariances
-    for (int e = tid; e < K1 * 9; e += 256) d.Xacc[(size_t)b * K1 * 9 + e] = Xs[e];
-    for (int e = tid; e < N * NU; e += 256) d.Uacc[(size_t)b * N * NU + e] = Us[e];
-    for (int e = tid; e < N * NU * 9; e += 256) d.Kacc[(size_t)b * N * NU * 9 + e] = d.K[(size_t)b * N * NU * 9 + e];
-    for (int e = tid; e < K1 * 81; e += 256) d.Sacc[(size_t)b * K1 * 81 + e] = d.Sig[(size_t)b * K1 * 81 + e];
+    for (int e = tid; e < K1 * 9; e += ACC_NT) d.Xacc[(size_t)b * K1 * 9 + e] = Xs[e];
+    for (int e = tid; e < N * NU; e += ACC_NT) d.Uacc[(size_t)b * N * NU + e] = Us[e];
+    for (int e = tid; e < N * NU * 9; e += ACC_NT) d.Kacc[(size_t)b * N * NU * 9 + e] = d.K[(size_t)b * N * NU * 9 + e];
+    for (int e = tid; e < K1 * 81; e += ACC_NT) d.Sacc[(size_t)b * K1 * 81 + e] = d.Sig[(size_t)b * K1 * 81 + e];
     if (d.scp_mode == CMPC_SCP_MODE_GUSTO) {   // the accepted solution becomes the linearization point
-        for (int e = tid; e < K1 * 9; e += 256) Xb[e] = Xs[e];
-        for (int e = tid; e < N * NU; e += 256) Ub[e] = Us[e];
+        for (int e = tid; e < K1 * 9; e += ACC_NT) Xb[e] = Xs[e];
+        for (int e = tid; e < N * NU; e += ACC_NT) Ub[e] = Us[e];
     }
 }
 
