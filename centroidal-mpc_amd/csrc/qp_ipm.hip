@@ -221,6 +221,10 @@ template <typename T, int ROBOT> struct Ctx {
     __device__ SV<T> var_u(int k) const { return kv(Ws<ROBOT>::u, k); }
 };
 
+// The Schur diagonal blocks S_jj and their inverses I_j are symmetric and stored packed (lower
+// triangle, row-major: (i, j), j <= i at i (i + 1) / 2 + j; 45 of a block's 81 slots)
+__device__ __forceinline__ int pk9(int i, int j) { return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i; }
+
 // 3x3 symmetric packed (00,10,11,20,21,22) helpers
 template <typename T> __device__ __forceinline__ T sym3(const T *p, int i, int j) {
     if (i < j) { int t = i; i = j; j = t; }
@@ -726,14 +730,14 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_sblock(const C
         T *Sd = C.Sd, *So = C.So;
         for (int i = 0; i < 9; ++i)
             for (int j = 0; j < 9; ++j) {
-                Sd[i * 9 + j] = Mfull(f0, i, j);
+                if (j <= i) Sd[pk9(i, j)] = Mfull(f0, i, j);
                 So[i * 9 + j] = MAt(f0, w, i, j);
             }
     }
     if (k == N) {
         T *Sd = C.Sd + (size_t)(N + 1) * 81;
         for (int i = 0; i < 9; ++i)
-            for (int j = 0; j < 9; ++j) Sd[i * 9 + j] = Mfull(f0, i, j);
+            for (int j = 0; j <= i; ++j) Sd[pk9(i, j)] = Mfull(f0, i, j);
         return;
     }
     const T Wm[3][3] = {{0, -w[2], w[1]}, {w[2], 0, -w[0]}, {-w[1], w[0], 0}};
@@ -786,8 +790,11 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_sblock(const C
     // + M_{k+1}
     for (int i = 0; i < 9; ++i)
         for (int j = 0; j < 9; ++j) Sm[i][j] += Mfull(f1, i, j);
-    T *Sd = C.Sd + (size_t)(1 + k) * 81;
-    for (int e = 0; e < 81; ++e) Sd[e] = Sm[e / 9][e % 9];
+    T *Sd = C.Sd + (size_t)(1 + k) * 81;   // packed lower triangle
+#pragma unroll
+    for (int i = 0; i < 9; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j) Sd[i * (i + 1) / 2 + j] = Sm[i][j];
     T *So = C.So + (size_t)(1 + k) * 81;
     if (k + 1 < N) {
         for (int i = 0; i < 9; ++i)
@@ -804,7 +811,7 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_sblock(const C
 //   top    (j < m):  X_j = S_{j,j-1} I_{j-1},  I_j = (S_jj - X_j S_{j-1,j})^-1      So[j-1] <- X_j
 //   bottom (j > m):  Y_j = S_{j,j+1} I_{j+1},  I_j = (S_jj - Y_j S_{j+1,j})^-1      So[j]   <- Y_j
 //   meet   (j = m):  I_m = (S_mm - X_m S_{m-1,m} - Y_m S_{m+1,m})^-1
-// Sd[j] holds S_jj on input and I_j on output, So[j] holds S_{j,j+1} on input (both in the
+// Sd[j] holds S_jj on input and I_j on output (packed, pk9), So[j] holds S_{j,j+1} on input (both in the
 // workspace, so the kernel's LDS stays small and several problems share a CU).  Each half-wave
 // keeps its previous inverse and the step's blocks in a small LDS scratch; the next step's raw
 // blocks are fetched one step ahead (a step is thousands of cycles).  Inverses by Gauss-Jordan
@@ -941,7 +948,7 @@ __device__ __forceinline__ void tw_step(const LdsT<T> *Dn, const LdsT<T> *Op, co
 #pragma unroll
     for (int q = 0; q < NE; ++q) {
         P[e[q]] = a[q];
-        if (ok[q]) Iout[e[q]] = a[q];
+        if (ok[q] && ii[q] >= cc[q]) Iout[ii[q] * (ii[q] + 1) / 2 + cc[q]] = a[q];   // packed
     }
     if (vb) {
         if (Op && Oq) {   // meeting block: x_m = I_m (b_m - X_m y_{m-1} - Y_m y_{m+1})
@@ -971,13 +978,14 @@ __device__ void tw_factor_ends(T *Sd, T *So, int NB, int m, LdsT<T> *sh, LdsT<T>
     LdsT<T> *A = sh + (top ? 0 : TW_SCRATCH), *P = A + 88, *Xb = A + 176, *Ob = A + 264, *Dd = A + 352,
             *Dn = A + 368;
     const int j0 = top ? 0 : NB - 1, dj = top ? 1 : -1, nstep = top ? m : NB - 1 - m;
-    int e[NE], et[NE];
+    int e[NE], et[NE], ep[NE];
     bool ok[NE];
 #pragma unroll
     for (int q = 0; q < NE; ++q) {
         ok[q] = l + 32 * q < 81;
         e[q] = ok[q] ? l + 32 * q : 80;
         et[q] = top ? e[q] : (e[q] % 9) * 9 + e[q] / 9;   // landing slot of a coupling element
+        ep[q] = pk9(e[q] / 9, e[q] % 9);                   // packed slot of a diagonal-block element
     }
     unsigned long long sub[4] = {0, 0, 0, 0};
     unsigned long long *subp = (stamp_out && top) ? sub : nullptr;
@@ -985,7 +993,7 @@ __device__ void tw_factor_ends(T *Sd, T *So, int NB, int m, LdsT<T> *sh, LdsT<T>
         const T *D0 = Sd + (size_t)j0 * 81;
         T v[NE];
 #pragma unroll
-        for (int q = 0; q < NE; ++q) v[q] = D0[e[q]];
+        for (int q = 0; q < NE; ++q) v[q] = D0[ep[q]];
 #pragma unroll
         for (int q = 0; q < NE; ++q) Dn[e[q]] = v[q];
     }
@@ -997,7 +1005,7 @@ __device__ void tw_factor_ends(T *Sd, T *So, int NB, int m, LdsT<T> *sh, LdsT<T>
         const T *On = So + (size_t)(top ? (jn > 0 ? jn - 1 : 0) : jn) * 81, *Dnx = Sd + (size_t)jn * 81;
         T pv[NE], nv[NE];
 #pragma unroll
-        for (int q = 0; q < NE; ++q) { pv[q] = On[e[q]]; nv[q] = Dnx[e[q]]; }
+        for (int q = 0; q < NE; ++q) { pv[q] = On[e[q]]; nv[q] = Dnx[ep[q]]; }
         if (act) {
             if (s == 0)
                 tw_step<T, 32>(Dn, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, Sd + (size_t)j * 81, A, P,
@@ -1031,8 +1039,8 @@ template <typename T> __device__ void tw_factor_meet(T *Sd, T *So, int m, LdsT<T
     Oq[e0] = So[(size_t)m * 81 + e0];
     if (has1) { Op[e1] = So[(size_t)(m - 1) * 81 + e1]; Oq[e1] = So[(size_t)m * 81 + e1]; }
     LdsT<T> *Dn = A + 368;
-    Dn[e0] = Sd[(size_t)m * 81 + e0];
-    if (has1) Dn[e1] = Sd[(size_t)m * 81 + e1];
+    Dn[e0] = Sd[(size_t)m * 81 + pk9(e0 / 9, e0 % 9)];
+    if (has1) Dn[e1] = Sd[(size_t)m * 81 + pk9(e1 / 9, e1 % 9)];
     wave_sync();
     tw_step<T, 64>(Dn, Op, P, Oq, Pq, So + (size_t)(m - 1) * 81, So + (size_t)m * 81, Sd + (size_t)m * 81, A, P,
                    Xb, Dd, vb, m, m - 1, m + 1);
@@ -1046,7 +1054,7 @@ template <typename T> __device__ void tw_factor_meet(T *Sd, T *So, int m, LdsT<T
 // compiler's wait counting would drain the queue), and the loads are branch-free (a clamped
 // index past the end re-reads the last block).
 constexpr int RSLOT = 88;
-template <typename T, int K> struct ChunkStream {
+template <typename T, int K, bool PK = false> struct ChunkStream {   // PK: packed symmetric blocks
     const T *base;   // block i at base + i * step
     long step;
     int n;
@@ -1059,7 +1067,10 @@ template <typename T, int K> struct ChunkStream {
             const int i = c * K + q;
             const T *p = base + (i < n ? i : n - 1) * step;
 #pragma unroll
-            for (int g = 0; g < 3; ++g) r[q][g] = p[l + 32 * g < 81 ? l + 32 * g : 80];
+            for (int g = 0; g < 3; ++g) {
+                const int el = l + 32 * g < 81 ? l + 32 * g : 80;
+                r[q][g] = p[PK ? pk9(el / 9, el % 9) : el];
+            }
         }
     }
     __device__ __forceinline__ void land(int c) {
@@ -1132,9 +1143,9 @@ __device__ void tw_solve_meet(const T *Ii, const T *Xs, int NB, int m, LdsT<T> *
     }
     wave_sync();
     if (lane < 9) {
-        const T *I = Ii + (size_t)m * 81 + lane * 9;
+        const T *I = Ii + (size_t)m * 81;   // packed
         T v = T(0);
-        for (int q = 0; q < 9; ++q) v = fma(I[q], sh[q], v);
+        for (int q = 0; q < 9; ++q) v = fma(I[pk9(lane, q)], sh[q], v);
         vb[m * 9 + lane] = v;
     }
     wave_sync();
@@ -1146,7 +1157,7 @@ __device__ void tw_solve_back(const T *Ii, const T *Xs, int NB, int m, LdsT<T> *
     const int lr = l < 9 ? l : 0;
     // step i: top j = m - 1 - i (I_j, X_{j+1} at So[j]); bottom j = m + 1 + i (I_j, Y_{j-1} at So[j-1])
     const int n = top ? m : NB - 1 - m, nmax = m;
-    ChunkStream<T, KB> I{Ii + (size_t)(top ? m - 1 : m + 1) * 81, top ? -81L : 81L, n > 0 ? n : 1, ring, {}};
+    ChunkStream<T, KB, true> I{Ii + (size_t)(top ? m - 1 : m + 1) * 81, top ? -81L : 81L, n > 0 ? n : 1, ring, {}};
     ChunkStream<T, KB> X{Xs + (size_t)(top ? m - 1 : m) * 81, top ? -81L : 81L, n > 0 ? n : 1, ring + 2 * KB * RSLOT, {}};
     I.issue(0);
     X.issue(0);
