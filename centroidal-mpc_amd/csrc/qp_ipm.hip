@@ -964,6 +964,129 @@ __device__ __forceinline__ void tw_step(const LdsT<T> *Dn, const LdsT<T> *Op, co
 #undef SUBSTAMP
 }
 
+// One end's step on a half-wave with the symmetric structure used (the ends' counterpart of
+// tw_step<T, 32>): X = Op' I_{j-1} is formed whole (81 elements, three per lane: it is not
+// symmetric), A = S_jj - X Op and its Gauss-Jordan inverse only on the upper triangle (45
+// elements, two per lane).  Gauss-Jordan on a symmetric matrix keeps A[j][i] = A[i][j] while i
+// and j are both pivoted or both not, and A[j][i] = -A[i][j] while exactly one is: at pivot c an
+// element reads A[i][c] = U[min(i,c)][max(i,c)] and A[c][j] = (c > j ? -1 : 1) U[min][max] from
+// the stored upper triangle U.  The inverse is mirrored into P (full, for the next step) and
+// stored packed into Iout.
+template <typename T>
+__device__ __forceinline__ void tw_step_sym(const LdsT<T> *Dn, const LdsT<T> *Op, const LdsT<T> *Ip, T *Xout, T *Iout,
+                                            LdsT<T> *A, LdsT<T> *P, LdsT<T> *Xb, LdsT<T> *Dd, LdsT<T> *vb, int j,
+                                            int jx, unsigned long long *sub = nullptr) {
+#ifdef CMPC_STAMPS
+    unsigned long long tq = __builtin_amdgcn_s_memtime();
+#define SUBSTAMP(i) do { if (sub) { const unsigned long long tn = __builtin_amdgcn_s_memtime(); sub[i] += tn - tq; tq = tn; } } while (0)
+#else
+#define SUBSTAMP(i) do { } while (0)
+#endif
+    const int l = threadIdx.x & 31;
+    // X elements (all 81): e = l + 32 q, clamped to 80 past the end (bit-identical duplicates)
+    int e[3], ii[3], cc[3];
+    bool ok[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        ok[q] = l + 32 * q < 81;
+        e[q] = ok[q] ? l + 32 * q : 80;
+        ii[q] = e[q] / 9;
+        cc[q] = e[q] % 9;
+    }
+    // upper-triangle elements u = l + 32 q (row-major over i <= j), clamped to 44 = (8, 8)
+    int iu[2], ju[2];
+    bool oku[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        oku[q] = l + 32 * q < 45;
+        int r = oku[q] ? l + 32 * q : 44, row = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {   // walk the rows (lengths 9, 8, ..., 1)
+            const bool past = r >= 9 - i && row == i;
+            r = past ? r - (9 - i) : r;
+            row = past ? i + 1 : row;
+        }
+        iu[q] = row;
+        ju[q] = row + r;
+    }
+    T au[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        au[q] = Dn[iu[q] * 9 + ju[q]];
+        if (iu[q] == ju[q]) Dd[iu[q]] = au[q];   // original diagonal (pivot floor)
+    }
+    T rv = (vb && l < 9) ? vb[j * 9 + l] : T(0);   // b_j (fused elimination)
+    auto dot = [&](auto fa, auto fb) -> T {
+        T u[9], v[9];
+#pragma unroll
+        for (int m = 0; m < 9; ++m) { u[m] = fa(m); v[m] = fb(m); }
+        T s0 = u[0] * v[0], s1 = u[1] * v[1], s2 = u[2] * v[2];
+#pragma unroll
+        for (int m = 3; m < 9; m += 3) { s0 = fma(u[m], v[m], s0); s1 = fma(u[m + 1], v[m + 1], s1); s2 = fma(u[m + 2], v[m + 2], s2); }
+        return s0 + s1 + s2;
+    };
+    if (Op) {   // X = Op' I_{j-1} (whole);  A -= X Op (upper triangle)
+        T x[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+            x[q] = dot([&](int m) { return Op[m * 9 + ii[q]]; }, [&](int m) { return Ip[m * 9 + cc[q]]; });
+#pragma unroll
+        for (int q = 0; q < 3; ++q) Xb[e[q]] = x[q];
+        wave_sync();
+        if (vb && l < 9) rv -= dot9(Xb + l * 9, vb + jx * 9);
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+            au[q] -= dot([&](int m) { return Xb[iu[q] * 9 + m]; }, [&](int m) { return Op[m * 9 + ju[q]]; });
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+            if (ok[q]) Xout[e[q]] = x[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) A[iu[q] * 9 + ju[q]] = au[q];
+    wave_sync();
+    SUBSTAMP(0);
+    T ip = rcp_nr(fmax(A[0], T(1e-13) * Dd[0]));
+#pragma unroll
+    for (int c = 0; c < 9; ++c) {
+        T aic[2], acj[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int i = iu[q], jj = ju[q];
+            const T v1 = A[min(i, c) * 9 + max(i, c)], v2 = A[min(c, jj) * 9 + max(c, jj)];
+            aic[q] = v1;
+            acj[q] = c > jj ? -v2 : v2;
+        }
+        T ipn = T(0);
+        if (c < 8) {   // A'[c+1][c+1] = U[c+1][c+1] - U[c][c+1]^2 / p_c (both indices unpivoted)
+            const T ncc = A[(c + 1) * 9 + c + 1], nci = A[c * 9 + c + 1];
+            ipn = rcp_nr(fmax(fma(-(nci * ip), nci, ncc), T(1e-13) * Dd[c + 1]));
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const T mi = aic[q] * ip;
+            const T gen = fma(-mi, acj[q], au[q]), row = acj[q] * ip, col = -mi;
+            const bool ic = __builtin_unpredictable(iu[q] == c), jc = __builtin_unpredictable(ju[q] == c);
+            au[q] = ic ? (jc ? ip : row) : (jc ? col : gen);
+        }
+        wave_sync();
+#pragma unroll
+        for (int q = 0; q < 2; ++q) A[iu[q] * 9 + ju[q]] = au[q];
+        wave_sync();
+        ip = ipn;
+    }
+    SUBSTAMP(1);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        P[iu[q] * 9 + ju[q]] = au[q];
+        P[ju[q] * 9 + iu[q]] = au[q];
+        if (oku[q]) Iout[ju[q] * (ju[q] + 1) / 2 + iu[q]] = au[q];   // packed (row ju >= column iu)
+    }
+    if (vb && l < 9) vb[j * 9 + l] = rv;
+    wave_sync();
+    SUBSTAMP(2);
+#undef SUBSTAMP
+}
+
 // the two ends, one per half-wave: lanes 0..31 the top blocks 0..m-1, lanes 32..63 the bottom
 // blocks NB-1..m+1 (for even NB the top end has one step more; the bottom half idles in it).
 // The raw blocks of step s + 1 are loaded during step s and landed in LDS at its end, inside
@@ -1008,11 +1131,10 @@ __device__ void tw_factor_ends(T *Sd, T *So, int NB, int m, LdsT<T> *sh, LdsT<T>
         for (int q = 0; q < NE; ++q) { pv[q] = On[e[q]]; nv[q] = Dnx[ep[q]]; }
         if (act) {
             if (s == 0)
-                tw_step<T, 32>(Dn, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, Sd + (size_t)j * 81, A, P,
-                               Xb, Dd, vb, j, 0, 0, subp);
+                tw_step_sym<T>(Dn, nullptr, nullptr, nullptr, Sd + (size_t)j * 81, A, P, Xb, Dd, vb, j, 0, subp);
             else
-                tw_step<T, 32>(Dn, Ob, P, nullptr, nullptr, So + (size_t)(top ? j - 1 : j) * 81, nullptr,
-                               Sd + (size_t)j * 81, A, P, Xb, Dd, vb, j, j - dj, 0, subp);
+                tw_step_sym<T>(Dn, Ob, P, So + (size_t)(top ? j - 1 : j) * 81, Sd + (size_t)j * 81, A, P, Xb, Dd, vb,
+                               j, j - dj, subp);
         }
 #ifdef CMPC_STAMPS
         const unsigned long long tl = __builtin_amdgcn_s_memtime();
