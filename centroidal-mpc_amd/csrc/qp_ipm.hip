@@ -563,23 +563,33 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_residual(const
 }
 
 // (2) Phi factors of knot k
-template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_factor(const Ctx<T, ROBOT> &C, int k) {
+// s, lambda and the friction rows G of knot k: loaded once for the Phi factors and the
+// predictor's w, which run back to back on the same knot (the factor stores in between would
+// otherwise force w to reload them)
+template <typename T, int ROBOT> struct KnotSL {
+    T s[Rows<ROBOT>::NI], l[Rows<ROBOT>::NI], G[Robot<ROBOT>::NC][12];
+};
+template <typename T, int ROBOT> __device__ __forceinline__ void load_knot_sl(const Ctx<T, ROBOT> &C, int k, KnotSL<T, ROBOT> &kl) {
     using S = Stage<ROBOT>;
+    constexpr int NC = Robot<ROBOT>::NC;
+    ldv(C.kv(WF(s), k), kl.s);
+    ldv(C.kv(WF(l), k), kl.l);
+    const auto st = C.st(k < C.N ? k : 0);
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int e = 0; e < 12; ++e) kl.G[c][e] = st[S::CON + S::CS * c + S::G + e];
+}
+
+template <typename T, int ROBOT>
+__device__ __forceinline__ void phase_factor(const Ctx<T, ROBOT> &C, int k, const KnotSL<T, ROBOT> &kl) {
     using R_ = Rows<ROBOT>;
-    constexpr int NI = R_::NI, NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
+    constexpr int NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
     const int N = C.N;
     const DevParams<T> &P = *C.prm;
-    T s[NI], lm[NI];
-    ldv(C.kv(WF(s), k), s);
-    ldv(C.kv(WF(l), k), lm);
+    const T *s = kl.s, *lm = kl.l;
     const unsigned msk = C.cmask(k);
-    // friction rows of every contact, loaded before the first factor store
-    T Gr[NC][12];
-    {
-        const auto st = C.st(k < N ? k : 0);
-        for (int c = 0; c < NC; ++c)
-            for (int e = 0; e < 12; ++e) Gr[c][e] = st[S::CON + S::CS * c + S::G + e];
-    }
+    const auto &Gr = kl.G;
     const SV<T> fx = C.kv(WF(facx), k);
     // (L, t) block in push-through form (no D * r product, no cancellation as rows pin L or t),
     // see tr_factor; stored: M_LL = [Phi^-1]_LL = W_L^-1 - Z'Z + cw^2 g g' / den with
@@ -1345,16 +1355,16 @@ __device__ __forceinline__ void rhat_rows(const Ctx<T, ROBOT> &C, int k, int cor
 }
 
 // (5a) particular solution w = Phi^-1 (r_d + G' D rhat) (friction rows in push-through form)
-template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_w(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu) {
-    using S = Stage<ROBOT>;
+// getG(c, G): the friction rows of contact c (from registers in the predictor, which shares the
+// factor phase's loads, or from the stage record)
+template <typename T, int ROBOT, typename GF>
+__device__ __forceinline__ void phase_w_core(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu,
+                                             const T (&sv)[Rows<ROBOT>::NI], const T (&lv)[Rows<ROBOT>::NI], GF &&getG) {
     using R_ = Rows<ROBOT>;
     constexpr int NI = R_::NI, NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
     const int N = C.N;
     const bool hu = k < N;
     const DevParams<T> &P = *C.prm;
-    T sv[NI], lv[NI];
-    ldv(C.kv(WF(s), k), sv);
-    ldv(C.kv(WF(l), k), lv);
     T rh[NI];
     rhat_rows(C, k, corr, sigma_mu, sv, lv, rh);   // kept for phase_dz (stored below)
     T rdx[9], rdu[NU];
@@ -1383,13 +1393,12 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_w(const Ctx<T,
                     vu[NUPC * c + dd] += C.Dform(lv[r0], sv[r0]) * rh[r0] - C.Dform(lv[r0 + 1], sv[r0 + 1]) * rh[r0 + 1];
                 }
         }
-        const auto st = C.st(k);
         const unsigned msk = C.cmask(k);
 #pragma unroll
         for (int c = 0; c < NC; ++c) {   // Phi_u^-1 (vu + G' D rhat) contact by contact
             const bool act = (msk >> c) & 1u;
             T G[12];
-            ldv(st + (S::CON + S::CS * c + S::G), G);
+            getG(c, G);
             const T *Wc = P.Wu + NUPC * c;
             const T wi[3] = {T(1) / Wc[FO], T(1) / Wc[FO + 1], T(1) / Wc[FO + 2]};
             T Gw[4][3], Ki[10], F[6], wd[NUPC];
@@ -1418,6 +1427,21 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_w(const Ctx<T,
     C.kv(WF(wt), k)[0] = wt;
     if (hu) stv(C.kv(WF(wu), k), ou);
     stv(C.kv(WF(rh), k), rh);
+}
+template <typename T, int ROBOT> __device__ __forceinline__ void phase_w(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu) {
+    using S = Stage<ROBOT>;
+    constexpr int NI = Rows<ROBOT>::NI;
+    T sv[NI], lv[NI];
+    ldv(C.kv(WF(s), k), sv);
+    ldv(C.kv(WF(l), k), lv);
+    const auto st = C.st(k);
+    phase_w_core(C, k, corr, sigma_mu, sv, lv, [&](int c, T (&G)[12]) { ldv(st + (S::CON + S::CS * c + S::G), G); });
+}
+template <typename T, int ROBOT> __device__ __forceinline__ void phase_w_pred(const Ctx<T, ROBOT> &C, int k, const KnotSL<T, ROBOT> &kl) {
+    phase_w_core(C, k, 0, T(0), kl.s, kl.l, [&](int c, T (&G)[12]) {
+#pragma unroll
+        for (int e = 0; e < 12; ++e) G[e] = kl.G[c][e];
+    });
 }
 
 
@@ -1743,8 +1767,10 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
         // ---- Phi factors and the predictor's particular solution (knot-local), then the S blocks
         // and the predictor's Schur right-hand side
         for (int k = tid; k < K1; k += NT) {
-            phase_factor<T, ROBOT>(C, k);
-            phase_w<T, ROBOT>(C, k, 0, T(0));
+            KnotSL<T, ROBOT> kl;
+            load_knot_sl(C, k, kl);
+            phase_factor<T, ROBOT>(C, k, kl);
+            phase_w_pred<T, ROBOT>(C, k, kl);
         }
         __syncthreads();
         STAMP(1);
