@@ -435,12 +435,49 @@ __device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<
     const DevParams<T> &P = *C.prm;
     const SV<const T> st{stp};
     const unsigned msk = C.cmask(k);
-    T x[9], u[NU];
+    T x[9], u[NU], x1[9], nk[9], n1[9], w[3];
 #pragma unroll
-    for (int i = 0; i < 9; ++i) x[i] = xs[i * ld];
+    for (int i = 0; i < 9; ++i) {
+        x[i] = xs[i * ld];
+        x1[i] = xs[i * ld + 1];   // x_{k+1} (k = N: unused)
+        nk[i] = nus[i * ld];      // nu blocks k, k + 1
+        n1[i] = nus[i * ld + 1];
+    }
 #pragma unroll
     for (int i = 0; i < NU; ++i) u[i] = us[i * ld];   // k = N: padding column (values unused)
+    for (int i = 0; i < 3; ++i) w[i] = st[S::W + i];
     const T t = ts[0];
+    // E' nu at knot k (kept for the dual rows at the end)
+    T ex[9], eu[NU];
+    for (int i = 0; i < 9; ++i) ex[i] = (k == 0) ? nk[i] : -nk[i];
+    if (k == N) for (int i = 0; i < 9; ++i) ex[i] += n1[i];
+    if (hu) {
+        T a[9];
+        opAT(w, C.beta, n1, a);
+        for (int i = 0; i < 9; ++i) ex[i] += a[i];
+        opBT<T, ROBOT>(st, n1, eu);
+        // dynamics row block 1 + k first: its loads (x_{k+1}, r_k) are then dead before the rows
+        T ax[9], bu[9];
+        opA(w, C.beta, x, ax);
+        opB<T, ROBOT>(st, u, bu);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            const T ez = ax[i] + bu[i] - x1[i], r = st[S::R + i];
+            const T re = ez - r;
+            rde_o[i * ld + 1 + k] = re;
+            nm.prim = fmax(nm.prim, fabs(re));
+            nm.sp = fmax(nm.sp, fmax(fabs(ez), fabs(r)));
+        }
+    }
+    if (k == 0 || k == N) {   // boundary rows: block 0 (initial state) / N + 1 (final state)
+        const T *xb = C.xbar + (size_t)k * 9;
+        for (int i = 0; i < 9; ++i) {
+            const T rb = x[i] - xb[i];
+            rde_o[i * ld + (k == 0 ? 0 : N + 1)] = rb;
+            nm.prim = fmax(nm.prim, fabs(rb));
+            nm.sp = fmax(nm.sp, fmax(fabs(x[i]), fabs(xb[i])));
+        }
+    }
     // inequality rows: r_i = g'z - h + s, complementarity and norms; G' lambda accumulated on the fly
     T gL[3] = {T(0), T(0), T(0)}, gt = T(0), gu[NU];
 #pragma unroll
@@ -495,20 +532,6 @@ __device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<
         }
         nm.mu += mug;
     }
-    // E' nu at knot k
-    T nk[9], n1[9], ex[9], eu[NU];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) { nk[i] = nus[i * ld]; n1[i] = nus[i * ld + 1]; }   // nu blocks k, k + 1
-    for (int i = 0; i < 9; ++i) ex[i] = (k == 0) ? nk[i] : -nk[i];
-    if (k == N) for (int i = 0; i < 9; ++i) ex[i] += n1[i];
-    T w[3];
-    for (int i = 0; i < 3; ++i) w[i] = st[S::W + i];
-    if (hu) {
-        T a[9];
-        opAT(w, C.beta, n1, a);
-        for (int i = 0; i < 9; ++i) ex[i] += a[i];
-        opBT<T, ROBOT>(st, n1, eu);
-    }
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
         const T hx = P.Wx[i] * x[i], q = st[S::QX + i];
@@ -530,27 +553,6 @@ __device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<
             rdu_o[i * ld] = rd;
             nm.dual = fmax(nm.dual, fabs(rd));
             nm.sd = fmax(nm.sd, fmax(fabs(h), fmax(fabs(eu[i]), fabs(gu[i]))));
-        }
-        // dynamics row block 1 + k
-        T ax[9], bu[9];
-        opA(w, C.beta, x, ax);
-        opB<T, ROBOT>(st, u, bu);
-#pragma unroll
-        for (int i = 0; i < 9; ++i) {
-            const T ez = ax[i] + bu[i] - xs[i * ld + 1], r = st[S::R + i];   // x_{k+1}
-            const T re = ez - r;
-            rde_o[i * ld + 1 + k] = re;
-            nm.prim = fmax(nm.prim, fabs(re));
-            nm.sp = fmax(nm.sp, fmax(fabs(ez), fabs(r)));
-        }
-    }
-    if (k == 0 || k == N) {   // boundary rows: block 0 (initial state) / N + 1 (final state)
-        const T *xb = C.xbar + (size_t)k * 9;
-        for (int i = 0; i < 9; ++i) {
-            const T rb = x[i] - xb[i];
-            rde_o[i * ld + (k == 0 ? 0 : N + 1)] = rb;
-            nm.prim = fmax(nm.prim, fabs(rb));
-            nm.sp = fmax(nm.sp, fmax(fabs(x[i]), fabs(xb[i])));
         }
     }
 }
