@@ -211,3 +211,22 @@ def test_edge_single_problem_and_max_horizon():
     k = kkt_residuals(P, q, A, l, u, z[0], y[0])
     assert st[0] == 1 and k['prim'] <= 1e-8
     s.close()
+
+
+@pytest.mark.parametrize('cfg,N,B', [('trot', 31, 2), ('trot', 2, 2), ('trot', 255, 2), ('talos', 101, 2)])
+def test_qp_horizon_edges(cfg, N, B):
+    """Horizons at the edges of the half-wave Schur recurrence: odd N (N + 2 odd: both ends take
+    the same number of steps), the smallest horizon (N = 2: one step per end) and the largest
+    (N = 255: 257 blocks, the workspace pitch KPC).  KKT residuals of the reference-form QP."""
+    pb, s = _solver(cfg, N, B)
+    s.linearize(); s.assemble(); s.qp_solve()
+    z, y, st, it = s.qp_solution()
+    assert np.all(st == 1), st
+    for b in range(B):
+        P, q, A, l, u = s.export_qp(b)
+        k = kkt_residuals(P, q, A, l, u, z[b], y[b])
+        scale = max(1.0, np.abs(P @ z[b]).max(), np.abs(q).max())
+        assert k['prim'] <= 1e-8, k['prim']
+        assert k['dual'] <= 1e-6 * scale, (k['dual'], scale)
+        assert k['sign'] == 0.0
+    s.close()
