@@ -1517,6 +1517,11 @@ __device__ __forceinline__ T dz_knot(const Ctx<T, ROBOT> &C, int k, T (&mus)[3],
         const T qs = fdiv(-sr, dsr < T(0) ? dsr : T(-1)), ql = fdiv(-lr, dlr < T(0) ? dlr : T(-1));
         amax = fmin(amax, fmin(dsr < T(0) ? qs : T(1), dlr < T(0) ? ql : T(1)));
     };
+    // the knot's control-sized records, loaded with the (x, t) rows (per-contact loads next to
+    // their use were each waited on alone)
+    T wuv[NU], rduv[NU];
+#pragma unroll
+    for (int q = 0; q < NU; ++q) { wuv[q] = wup[q * ld]; rduv[q] = rdup[q * ld]; }
     // (x, t) part and the trust-region / slack rows
     {
         T rdx[9], s9[9], l9[9], rh9[9], ri9[9];
@@ -1573,10 +1578,10 @@ __device__ __forceinline__ T dz_knot(const Ctx<T, ROBOT> &C, int k, T (&mus)[3],
         // unconditional loads (kc keeps the addresses valid at k = N) masked by arithmetic: a
         // select on a loaded value becomes a branch around the load and a wait per row
         const T hf = hu ? T(1) : T(0);
-        for (int q = 0; q < NUPC; ++q) du[q] = (-wup[(NUPC * c + q) * ld] - au[q]) * hf;
+        for (int q = 0; q < NUPC; ++q) du[q] = (-wuv[NUPC * c + q] - au[q]) * hf;
         if (hu)
             for (int q = 0; q < NUPC; ++q) duo[(NUPC * c + q) * ld] = du[q];
-        for (int i = 0; i < 3; ++i) vf[i] = -(rdup[(NUPC * c + FO + i) * ld] + ec[FO + i]) * hf;
+        for (int i = 0; i < 3; ++i) vf[i] = -(rduv[NUPC * c + FO + i] + ec[FO + i]) * hf;
         T z[4];
         for (int r = 0; r < 4; ++r) z[r] = Gw[r][0] * vf[0] + Gw[r][1] * vf[1] + Gw[r][2] * vf[2] + rh4[r];
 #pragma unroll
