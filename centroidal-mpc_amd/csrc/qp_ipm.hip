@@ -146,6 +146,12 @@ template <typename T, int ROBOT> struct Ctx {
     T *Sd, *So;           // Schur diagonal blocks / inverses and couplings (workspace, see tw_factor_ends)
     LdsT<T> *vb;          // Schur rhs -> direction dnu, (N+2) x 9 block vector in LDS
     T dcap;               // cap on D = lambda/s for the CoP rows (D-form, folded into W_cop)
+    const LdsT<T> *wt;    // LDS copy of the cost weights: Wx | 1/Wx | Wu | 1/Wu (parameter loads
+                          // next to workspace stores were each waited on alone)
+    __device__ T Wx(int i) const { return wt[i]; }
+    __device__ T iWx(int i) const { return wt[9 + i]; }
+    __device__ T Wu(int i) const { return wt[18 + i]; }
+    __device__ T iWu(int i) const { return wt[18 + NU + i]; }
     __device__ T Dform(T l, T s_) const { return fmin(fdiv(l, s_), dcap); }
 
     __device__ SV<const T> st(int k) const { return SV<const T>{stage + k}; }
@@ -304,8 +310,7 @@ template <typename T> __device__ void chol8(T (&a)[36]) {
 template <typename T, int ROBOT>
 __device__ __forceinline__ void tr_factor(const Ctx<T, ROBOT> &C, const T *s, const T *lm, T (&Lk)[36], T (&z1)[8],
                                           T &iden, T &dsl) {
-    const DevParams<T> &P = *C.prm;
-    const T wl[3] = {T(1) / P.Wx[6], T(1) / P.Wx[7], T(1) / P.Wx[8]};
+    const T wl[3] = {C.iWx(6), C.iWx(7), C.iWx(8)};
     const T kfl = T(KFLOOR<T>) * T(8) * (wl[0] + wl[1] + wl[2]);
 #pragma unroll
     for (int j = 0; j < 8; ++j)
@@ -387,14 +392,13 @@ template <typename T, int ROBOT, typename SA>
 __device__ __forceinline__ void contact_wd(const Ctx<T, ROBOT> &C, int c, bool act, const SA &s, const SA &lm,
                                            T (&wd)[Robot<ROBOT>::NUPC]) {
     constexpr int NUPC = Robot<ROBOT>::NUPC;
-    const T *Wc = C.prm->Wu + NUPC * c;
 #pragma unroll
-    for (int q = 0; q < NUPC; ++q) wd[q] = T(1) / Wc[q];
+    for (int q = 0; q < NUPC; ++q) wd[q] = C.iWu(NUPC * c + q);
     if (ROBOT == 1) {
 #pragma unroll
         for (int dd = 0; dd < 2; ++dd) {
             const int r0 = Rows<ROBOT>::CP + 4 * c + 2 * dd;
-            const T v = T(1) / (Wc[dd] + C.Dform(lm[r0], s[r0]) + C.Dform(lm[r0 + 1], s[r0 + 1]));
+            const T v = T(1) / (C.Wu(NUPC * c + dd) + C.Dform(lm[r0], s[r0]) + C.Dform(lm[r0 + 1], s[r0 + 1]));
             wd[dd] = act ? v : wd[dd];
         }
     }
@@ -534,7 +538,7 @@ __device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<
     }
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
-        const T hx = P.Wx[i] * x[i], q = st[S::QX + i];
+        const T hx = C.Wx(i) * x[i], q = st[S::QX + i];
         const T g = (i >= 6) ? gL[i - 6] : T(0);
         const T rd = hx + q + ex[i] + g;
         rdx_o[i * ld] = rd;
@@ -548,7 +552,7 @@ __device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<
     if (hu) {
 #pragma unroll
         for (int i = 0; i < NU; ++i) {
-            const T h = P.Wu[i] * u[i];
+            const T h = C.Wu(i) * u[i];
             const T rd = h + eu[i] + gu[i];
             rdu_o[i * ld] = rd;
             nm.dual = fmax(nm.dual, fabs(rd));
@@ -588,7 +592,6 @@ __device__ __forceinline__ void phase_factor(const Ctx<T, ROBOT> &C, int k, cons
     using R_ = Rows<ROBOT>;
     constexpr int NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
     const int N = C.N;
-    const DevParams<T> &P = *C.prm;
     const T *s = kl.s, *lm = kl.l;
     const unsigned msk = C.cmask(k);
     const auto &Gr = kl.G;
@@ -596,7 +599,7 @@ __device__ __forceinline__ void phase_factor(const Ctx<T, ROBOT> &C, int k, cons
     // (L, t) block in push-through form (no D * r product, no cancellation as rows pin L or t),
     // see tr_factor; stored: M_LL = [Phi^-1]_LL = W_L^-1 - Z'Z + cw^2 g g' / den with
     // Z = L^-1 Y, g = Z' z1 (phase_sblock).  L, z1, den are recomputed where they are used.
-    const T wl[3] = {T(1) / P.Wx[6], T(1) / P.Wx[7], T(1) / P.Wx[8]};
+    const T wl[3] = {C.iWx(6), C.iWx(7), C.iWx(8)};
     T Lk[36], z1[8], iden, dsl;
     tr_factor(C, s, lm, Lk, z1, iden, dsl);
     T Z[8][3];
@@ -623,17 +626,16 @@ __device__ __forceinline__ void phase_factor(const Ctx<T, ROBOT> &C, int k, cons
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         const SV<T> fu = C.kv(WF(facu), k) + c * FU;
-        const T *Wc = P.Wu + NUPC * c;
         const bool act = (msk >> c) & 1u;
         // Winvd: inverse diagonal of W' (CoP rows fold into their coordinate's diagonal)
-        for (int q = 0; q < NUPC; ++q) fu[FU_WI + q] = T(1) / Wc[q];
+        for (int q = 0; q < NUPC; ++q) fu[FU_WI + q] = C.iWu(NUPC * c + q);
         if (ROBOT == 1 && act) {
             for (int dd = 0; dd < 2; ++dd) {
                 const int r0 = R_::CP + 4 * c + 2 * dd;
-                fu[FU_WI + dd] = T(1) / (Wc[dd] + C.Dform(lm[r0], s[r0]) + C.Dform(lm[r0 + 1], s[r0 + 1]));
+                fu[FU_WI + dd] = T(1) / (C.Wu(NUPC * c + dd) + C.Dform(lm[r0], s[r0]) + C.Dform(lm[r0 + 1], s[r0 + 1]));
             }
         }
-        const T wi[3] = {T(1) / Wc[FO], T(1) / Wc[FO + 1], T(1) / Wc[FO + 2]};
+        const T wi[3] = {C.iWu(NUPC * c + FO), C.iWu(NUPC * c + FO + 1), C.iWu(NUPC * c + FO + 2)};
         if (!act) {
             fu[FU_F] = wi[0]; fu[FU_F + 1] = T(0); fu[FU_F + 2] = wi[1]; fu[FU_F + 3] = T(0); fu[FU_F + 4] = T(0); fu[FU_F + 5] = wi[2];
             continue;
@@ -655,7 +657,7 @@ __device__ __forceinline__ void phase_factor(const Ctx<T, ROBOT> &C, int k, cons
 template <typename T, int ROBOT>
 __device__ __forceinline__ void tr_local(const Ctx<T, ROBOT> &C, const T (&Lk)[36], const T (&z1)[8], T fdsl, T fden,
                                          const T *vL, T vt, const T *rh, T *dL, T &dt, T *dlt, T &dls) {
-    const T wl[3] = {rcp_nr(C.prm->Wx[6]), rcp_nr(C.prm->Wx[7]), rcp_nr(C.prm->Wx[8])};
+    const T wl[3] = {rcp_nr(C.Wx(6)), rcp_nr(C.Wx(7)), rcp_nr(C.Wx(8))};
     T y[8];
     for (int j = 0; j < 8; ++j) {
         T v = rh[j];
@@ -691,7 +693,7 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_sblock(const C
     const bool hu = k < N;
     // loads: M_k, M_{k+1} (1/Wx[0:6] | M_LL packed), the stage's A/B data, the contacts' F, W'^-1
     T f0[12], f1[12];
-    for (int i = 0; i < 6; ++i) f0[i] = f1[i] = T(1) / C.prm->Wx[i];
+    for (int i = 0; i < 6; ++i) f0[i] = f1[i] = C.iWx(i);
     {
         T m0[6], m1[6];
         ldv(C.kv(WF(facx), k) + FX_ML, m0);
@@ -1366,7 +1368,6 @@ __device__ __forceinline__ void phase_w_core(const Ctx<T, ROBOT> &C, int k, int 
     constexpr int NI = R_::NI, NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
     const int N = C.N;
     const bool hu = k < N;
-    const DevParams<T> &P = *C.prm;
     T rh[NI];
     rhat_rows(C, k, corr, sigma_mu, sv, lv, rh);   // kept for phase_dz (stored below)
     T rdx[9], rdu[NU];
@@ -1374,7 +1375,7 @@ __device__ __forceinline__ void phase_w_core(const Ctx<T, ROBOT> &C, int k, int 
     ldv(C.kv(WF(rdu), k), rdu);   // k = N: unused
     const T rdt = C.kv(WF(rdt), k)[0];
     T wx[9], wt;
-    for (int i = 0; i < 6; ++i) wx[i] = (T(1) / P.Wx[i]) * rdx[i];
+    for (int i = 0; i < 6; ++i) wx[i] = C.iWx(i) * rdx[i];
     {   // (L, t): w = -(local solve with v = -r_d)
         T Lk[36], z1[8], iden, dsl;
         tr_factor(C, sv, lv, Lk, z1, iden, dsl);
@@ -1401,8 +1402,7 @@ __device__ __forceinline__ void phase_w_core(const Ctx<T, ROBOT> &C, int k, int 
             const bool act = (msk >> c) & 1u;
             T G[12];
             getG(c, G);
-            const T *Wc = P.Wu + NUPC * c;
-            const T wi[3] = {T(1) / Wc[FO], T(1) / Wc[FO + 1], T(1) / Wc[FO + 2]};
+            const T wi[3] = {C.iWu(NUPC * c + FO), C.iWu(NUPC * c + FO + 1), C.iWu(NUPC * c + FO + 2)};
             T Gw[4][3], Ki[10], F[6], wd[NUPC];
             fric_factor(G, wi, sv + R_::FR + 4 * c, lv + R_::FR + 4 * c, act, Gw, Ki);
             fric_F(Gw, Ki, wi, F);
@@ -1535,7 +1535,7 @@ __device__ __forceinline__ T dz_knot(const Ctx<T, ROBOT> &C, int k, T (&mus)[3],
         }
         const T rdt = rdtp[0];
         T dx[9], dtt, dlt[8], dls;
-        for (int i = 0; i < 6; ++i) dx[i] = -(T(1) / C.prm->Wx[i]) * (rdx[i] + ex[i]);
+        for (int i = 0; i < 6; ++i) dx[i] = -C.iWx(i) * (rdx[i] + ex[i]);
         {
             T Lk[36], z1[8], iden, dsl;
             tr_factor(C, s9, l9, Lk, z1, iden, dsl);
@@ -1562,8 +1562,7 @@ __device__ __forceinline__ T dz_knot(const Ctx<T, ROBOT> &C, int k, T (&mus)[3],
             const int row = R_::FR + 4 * c + r;
             s4[r] = ss[row * ld]; l4[r] = ls[row * ld]; rh4[r] = rhp[row * ld]; ri4[r] = rdip[row * ld];
         }
-        const T *Wc = C.prm->Wu + NUPC * c;
-        const T wi[3] = {T(1) / Wc[FO], T(1) / Wc[FO + 1], T(1) / Wc[FO + 2]};
+        const T wi[3] = {C.iWu(NUPC * c + FO), C.iWu(NUPC * c + FO + 1), C.iWu(NUPC * c + FO + 2)};
         T Gw[4][3], Ki[10], F[6], wd[NUPC], au[NUPC], du[NUPC];
         fric_factor(G, wi, s4, l4, pr, Gw, Ki);
         fric_F(Gw, Ki, wi, F);
@@ -1692,7 +1691,7 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
     __shared__ T red[8 * (NT / 64)];
     __shared__ T sh[2 * TW_SCRATCH];
     const int tid = threadIdx.x, N = d.N, K1 = N + 1, NB = N + 2, NBm = NB / 2;
-    Ctx<T, ROBOT> C{N, nullptr, nullptr, nullptr, nullptr, T(0), T(0), nullptr, nullptr, nullptr, nullptr, T(0)};
+    Ctx<T, ROBOT> C{N, nullptr, nullptr, nullptr, nullptr, T(0), T(0), nullptr, nullptr, nullptr, nullptr, T(0), nullptr};
     C.prm = d.params + d.class_id[b];
     C.stage = d.stage + (size_t)b * Stage<ROBOT>::SIZE * KPC;
     C.logic = d.logic + (size_t)b * N * Robot<ROBOT>::NC;
@@ -1705,6 +1704,11 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
         C.dcap = T(1e12) * wmax;
     }
     C.ws = d.ws + (size_t)b * d.ws_stride;
+    __shared__ T wts[18 + 2 * NU];
+    if (tid < 9) { wts[tid] = C.prm->Wx[tid]; wts[9 + tid] = T(1) / C.prm->Wx[tid]; }
+    if (tid < NU) { wts[18 + tid] = C.prm->Wu[tid]; wts[18 + NU + tid] = T(1) / C.prm->Wu[tid]; }
+    C.wt = (const LdsT<T> *)wts;
+    __syncthreads();
     // dynamic LDS: the (N+2) x 9 Schur vector, then two block rings per wave for the sweeps
     LdsT<T> *shl = (LdsT<T> *)sh;
     C.vb = (LdsT<T> *)reinterpret_cast<T *>(dsmem);
