@@ -1654,20 +1654,60 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_update(const C
 
 // initialization step: full Newton step for z and nu; s = h - gz at the new z; lambda += dlambda.
 // vmax receives (max -s, max -lambda) over this knot's rows.
-template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_init_step(const Ctx<T, ROBOT> &C, int k, T (&vmax)[2]) {
-    constexpr int NI = Rows<ROBOT>::NI;
-    phase_update<T, ROBOT>(C, k, T(1), true);   // z, nu, lambda: full affine step; s recomputed below
-    T x[9], u[NU];
-    ldv(C.var_x(k), x);
-    ldv(C.var_u(k), u);   // k = N: rows of u are absent (values unused)
-    const T t = C.kv(WF(t), k)[0];
-    const SV<T> s = C.kv(WF(s), k), lm = C.kv(WF(l), k);
-    for (int r = 0; r < NI; ++r) {
-        if (!C.present(k, r)) continue;
-        s[r] = -C.gz(k, r, x, t, u, true);
-        vmax[0] = fmax(vmax[0], -s[r]);
-        vmax[1] = fmax(vmax[1], -lm[r]);
+// s = h - g'z at the new z for the present rows (absent rows keep s = 1: their affine step is
+// zero), branch-free with each row group's loads batched; restrict-qualified field pointers
+template <typename T, int ROBOT>
+__device__ __forceinline__ void init_s_knot(const Ctx<T, ROBOT> &C, int k, T (&vmax)[2], const T *__restrict__ stp,
+                                            const T *__restrict__ xs, const T *__restrict__ us,
+                                            const T *__restrict__ ts, T *__restrict__ ss, const T *__restrict__ ls) {
+    using S = Stage<ROBOT>;
+    using R_ = Rows<ROBOT>;
+    constexpr int NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
+    constexpr int ld = KPC;
+    const bool hu = k < C.N;
+    const SV<const T> st{stp};
+    const unsigned msk = C.cmask(k);
+    T x[3], u[NU];
+    for (int i = 0; i < 3; ++i) x[i] = xs[(6 + i) * ld];
+    for (int i = 0; i < NU; ++i) u[i] = us[i * ld];   // k = N: padding column (unused)
+    const T t = ts[0];
+    auto put = [&](int r, bool pr, T v) {   // v = g'z - h
+        ss[r * ld] = pr ? -v : T(1);
+        vmax[0] = fmax(vmax[0], pr ? v : T(-1e300));
+        vmax[1] = fmax(vmax[1], pr ? -ls[r * ld] : T(-1e300));
+    };
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        put(j, true, tr_sign<T>(j, 0) * x[0] + tr_sign<T>(j, 1) * x[1] + tr_sign<T>(j, 2) * x[2] + C.cw * t - st[S::BTR + j]);
+    put(8, true, -t);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const bool pr = hu && ((msk >> c) & 1u);
+        const auto cs = st + (S::CON + S::CS * c);
+        T G[12], H[4];
+        for (int e = 0; e < 12; ++e) G[e] = cs[S::G + e];
+        for (int r = 0; r < 4; ++r) H[r] = cs[S::H + r];
+        const T *f = u + NUPC * c + FO;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            put(R_::FR + 4 * c + r, pr, G[3 * r] * f[0] + G[3 * r + 1] * f[1] + G[3 * r + 2] * f[2] - H[r]);
+        if (ROBOT == 1) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {   // cop <= hi | -cop <= -lo
+                const int dd = q / 2;
+                const T cop = u[NUPC * c + dd];
+                put(R_::CP + 4 * c + q, pr,
+                    (q % 2 == 0) ? cop - C.prm->foot_range[dd == 0 ? 0 : 2] : -cop - C.prm->foot_range[dd == 0 ? 1 : 3]);
+            }
+        }
     }
+}
+
+template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_init_step(const Ctx<T, ROBOT> &C, int k, T (&vmax)[2]) {
+    phase_update<T, ROBOT>(C, k, T(1), true);   // z, nu, lambda: full affine step; s recomputed below
+    T *ws = C.ws;
+    init_s_knot<T, ROBOT>(C, k, vmax, C.stage + k, ws + WF(x) * KPC + k, ws + WF(u) * KPC + k, ws + WF(t) * KPC + k,
+                          ws + WF(s) * KPC + k, ws + WF(l) * KPC + k);
 }
 template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_init_shift(const Ctx<T, ROBOT> &C, int k, T sh_s, T sh_l) {
     constexpr int NI = Rows<ROBOT>::NI;
@@ -1730,10 +1770,13 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
     for (int k = tid; k < K1; k += NT) {
         const SV<T> x = C.var_x(k);
         const T *xl = d.Xlin + ((size_t)b * K1 + k) * 9;   // start at the linearization point
-        for (int i = 0; i < 9; ++i) x[i] = xl[i];
-        C.kv(WF(t), k)[0] = T(0);
         const T *ubar = d.Ulin + ((size_t)b * N + (k < N ? k : 0)) * NU;
-        if (k < N) { const SV<T> u = C.var_u(k); for (int i = 0; i < NU; ++i) u[i] = ubar[i]; }
+        T xv[9], uv[NU];   // loads first (interleaved with the stores they would be serialized)
+        for (int i = 0; i < 9; ++i) xv[i] = xl[i];
+        for (int i = 0; i < NU; ++i) uv[i] = ubar[i];
+        for (int i = 0; i < 9; ++i) x[i] = xv[i];
+        C.kv(WF(t), k)[0] = T(0);
+        if (k < N) { const SV<T> u = C.var_u(k); for (int i = 0; i < NU; ++i) u[i] = uv[i]; }
         const SV<T> s = C.kv(WF(s), k), lm = C.kv(WF(l), k), dsa = C.kv(WF(dsa), k), dla = C.kv(WF(dla), k);
         const unsigned msk = C.cmask(k);
         for (int r = 0; r < NI; ++r) {
