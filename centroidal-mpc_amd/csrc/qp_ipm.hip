@@ -1221,7 +1221,7 @@ template <typename T, int K, bool PK = false> struct ChunkStream {   // PK: pack
         return buf + ((i / K) & 1) * K * RSLOT + (i % K) * RSLOT;
     }
 };
-constexpr int KE = 8, KB = 4;   // chunk sizes of the elimination (one stream) and back (two) sweeps
+constexpr int KE = 8;   // blocks per chunk of the sweep streams
 constexpr int SWEEP_LDS = 2 * KE * RSLOT;   // per half-wave: 2 x 8 slots = 2 x (2 x 4) slots
 
 // (5c) two-ended block sweeps with the twisted factors (one end per half-wave): rhs -> dnu in
@@ -1286,46 +1286,62 @@ __device__ void tw_solve_meet(const T *Ii, const T *Xs, int NB, int m, LdsT<T> *
     }
     wave_sync();
 }
+// The back sweep's local terms z_j = I_j y_j for every block but the meeting one, all blocks in
+// parallel (thread per block, in place in vb) once the elimination and the meeting block are
+// done: the sequential step is then a single 9-term product.
+template <typename T> __device__ void tw_solve_local(const T *Ii, int NB, int m, LdsT<T> *vb) {
+    for (int j = threadIdx.x; j < NB; j += NT) {
+        if (j == m) continue;
+        const T *I = Ii + (size_t)j * 81;   // packed
+        T iv[45], y[9];
+#pragma unroll
+        for (int p = 0; p < 45; ++p) iv[p] = I[p];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) y[i] = vb[j * 9 + i];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            T a = iv[pk9(i, 0)] * y[0];
+#pragma unroll
+            for (int q = 1; q < 9; ++q) a = fma(iv[pk9(i, q)], y[q], a);
+            vb[j * 9 + i] = a;
+        }
+    }
+}
 template <typename T>
-__device__ void tw_solve_back(const T *Ii, const T *Xs, int NB, int m, LdsT<T> *vb, LdsT<T> *ring) {
+__device__ void tw_solve_back(const T *Xs, int NB, int m, LdsT<T> *vb, LdsT<T> *ring) {
     const int lane = threadIdx.x & 63, l = lane & 31;
     const bool top = lane < 32;
     const int lr = l < 9 ? l : 0;
-    // step i: top j = m - 1 - i (I_j, X_{j+1} at So[j]); bottom j = m + 1 + i (I_j, Y_{j-1} at So[j-1])
+    // step i: top j = m - 1 - i (X_{j+1} at So[j]); bottom j = m + 1 + i (Y_{j-1} at So[j-1]);
+    // vb[j] holds z_j = I_j y_j (tw_solve_local)
     const int n = top ? m : NB - 1 - m, nmax = m;
-    ChunkStream<T, KB, true> I{Ii + (size_t)(top ? m - 1 : m + 1) * 81, top ? -81L : 81L, n > 0 ? n : 1, ring, {}};
-    ChunkStream<T, KB> X{Xs + (size_t)(top ? m - 1 : m) * 81, top ? -81L : 81L, n > 0 ? n : 1, ring + 2 * KB * RSLOT, {}};
-    I.issue(0);
+    ChunkStream<T, KE> X{Xs + (size_t)(top ? m - 1 : m) * 81, top ? -81L : 81L, n > 0 ? n : 1, ring, {}};
     X.issue(0);
-    I.land(0);
     X.land(0);
-    for (int c = 0; c * KB < nmax; ++c) {
-        I.issue(c + 1);
+    for (int c = 0; c * KE < nmax; ++c) {
         X.issue(c + 1);
         wave_sync();
-        for (int q = 0; q < KB; ++q) {
-            const int i = c * KB + q;
+        for (int q = 0; q < KE; ++q) {
+            const int i = c * KE + q;
             if (i >= nmax) break;
             const int j = top ? m - 1 - i : m + 1 + i, jn = top ? j + 1 : j - 1;
             T v = T(0);
             const bool act = l < 9 && i < n;
             if (act) {
-                const LdsT<T> *ir = I.blk(i) + lr * 9;    // symmetric: row == column
                 const LdsT<T> *xb = X.blk(i);
-                const LdsT<T> *yv_ = vb + j * 9, *xn = vb + jn * 9;
-                T iv[9], yv[9], xc[9], nv[9];
+                const LdsT<T> *xn = vb + jn * 9;
+                T xc[9], nv[9];
 #pragma unroll
-                for (int e = 0; e < 9; ++e) { iv[e] = ir[e]; yv[e] = yv_[e]; xc[e] = xb[e * 9 + lr]; nv[e] = xn[e]; }
-                T s0 = iv[0] * yv[0], s1 = -(xc[0] * nv[0]);
+                for (int e = 0; e < 9; ++e) { xc[e] = xb[e * 9 + lr]; nv[e] = xn[e]; }
+                T s0 = vb[j * 9 + lr] - xc[0] * nv[0], s1 = -(xc[1] * nv[1]), s2 = -(xc[2] * nv[2]);
 #pragma unroll
-                for (int e = 1; e < 9; ++e) { s0 = fma(iv[e], yv[e], s0); s1 = fma(-xc[e], nv[e], s1); }
-                v = s0 + s1;
+                for (int e = 3; e < 9; e += 3) { s0 = fma(-xc[e], nv[e], s0); s1 = fma(-xc[e + 1], nv[e + 1], s1); s2 = fma(-xc[e + 2], nv[e + 2], s2); }
+                v = s0 + s1 + s2;
             }
             wave_sync();
             if (act) vb[j * 9 + l] = v;
             wave_sync();
         }
-        I.land(c + 1);
         X.land(c + 1);
     }
     wave_sync();
@@ -1860,7 +1876,9 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
                 if (tid < 64) tw_solve_meet<T>(C.Sd, C.So, NB, NBm, C.vb, shl);
                 __syncthreads();
             }
-            tw_solve_back<T>(C.Sd, C.So, NB, NBm, C.vb, ring);
+            tw_solve_local<T>(C.Sd, NB, NBm, C.vb);
+            __syncthreads();
+            tw_solve_back<T>(C.So, NB, NBm, C.vb, ring);
             __syncthreads();
             STAMP(6);
             T am[1] = {T(1)}, mus[3] = {T(0), T(0), T(0)};
