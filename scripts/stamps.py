@@ -22,7 +22,7 @@ _, _, _, itv = s.qp_solution(with_y=False)
 print('  ipm iterations of the last solve: mean %.2f  p50 %d  p90 %d  p99 %d  max %d' % (
     itv.mean(), np.percentile(itv, 50), np.percentile(itv, 90), np.percentile(itv, 99), itv.max()))
 tq = st[:, :9].sum(axis=1)
-print('  per-problem QP cycles (warm-up + timed): p50 %.3g  p90 %.3g  max %.3g' % (
+print('  per-problem QP cycles of the timed solve: p50 %.3g  p90 %.3g  max %.3g' % (
     np.percentile(tq, 50), np.percentile(tq, 90), tq.max()))
 for i, n in enumerate(names):
     print('  %-11s %5.1f%%  %.3g cycles/IPM-iter' % (n, 100 * st[:, i].mean() / tot, st[:, i].mean() / its))
