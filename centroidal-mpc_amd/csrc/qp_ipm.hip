@@ -159,7 +159,9 @@ template <typename T, int ROBOT> struct Ctx {
     __device__ SV<T> kv(int f, int k) const { return SV<T>{ws + f * KPC + k}; }
     __device__ SV<T> bv(int f, int j) const { return SV<T>{ws + f * KPC + j}; }
     // contact-active bits of knot k, loaded once per phase (0 at k = N: only the TR rows exist)
-    __device__ unsigned cmask(int k) const {
+    const LdsT<uint8_t> *cm = nullptr;   // per-knot contact masks in LDS (set once per solve)
+    __device__ unsigned cmask(int k) const { return cm ? unsigned(cm[k]) : cmask_mem(k); }
+    __device__ unsigned cmask_mem(int k) const {
         if (k >= N) return 0u;
         const uint8_t *lg = logic + (size_t)k * NC;
         unsigned m = 0;
@@ -1764,6 +1766,11 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
     if (tid < 9) { wts[tid] = C.prm->Wx[tid]; wts[9 + tid] = T(1) / C.prm->Wx[tid]; }
     if (tid < NU) { wts[18 + tid] = C.prm->Wu[tid]; wts[18 + NU + tid] = T(1) / C.prm->Wu[tid]; }
     C.wt = (const LdsT<T> *)wts;
+    // contact masks of every knot, once per solve (each phase read them from global memory
+    // first thing, and everything after waited on that load)
+    __shared__ uint8_t cms[KPC];
+    for (int k = tid; k < K1; k += NT) cms[k] = (uint8_t)C.cmask_mem(k);
+    C.cm = (const LdsT<uint8_t> *)cms;
     __syncthreads();
     // dynamic LDS: the (N+2) x 9 Schur vector, then two block rings per wave for the sweeps
     LdsT<T> *shl = (LdsT<T> *)sh;
