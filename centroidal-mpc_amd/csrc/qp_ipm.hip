@@ -1443,10 +1443,32 @@ __device__ __forceinline__ void phase_w_core(const Ctx<T, ROBOT> &C, int k, int 
         }
     }
     // stores
-    stv(C.kv(WF(wx), k), wx);
-    C.kv(WF(wt), k)[0] = wt;
+    (void)wt;   // w_x, w_t enter only the right-hand side below; w_u is read by phase_dz
     if (hu) stv(C.kv(WF(wu), k), ou);
     stv(C.kv(WF(rh), k), rh);
+    // the Schur right-hand side, fused: block 1 + k = r_k - A_k wx_k - B_k wu_k + wx_{k+1}.  Thread
+    // k writes all but the last term; after a wave-level fence (block k was written by lane k - 1
+    // in this pass or an earlier one: the lanes of the one wave run in lockstep) it adds its own
+    // wx_k to block k.  Block 0 = r_init - wx_0, block N + 1 = r_final - wx_N.
+    {
+        using S = Stage<ROBOT>;
+        LdsT<T> *vb = C.vb;
+        T r0[9], r1[9];
+        ldv(C.bv(WF(rde), k == N ? N + 1 : 0), r0);   // boundary rows (k = 0: init, k = N: final)
+        ldv(C.bv(WF(rde), hu ? 1 + k : 0), r1);       // dynamics rows of knot k
+        if (k == 0) for (int i = 0; i < 9; ++i) vb[i] = r0[i] - wx[i];
+        if (k == N) for (int i = 0; i < 9; ++i) vb[(N + 1) * 9 + i] = r0[i] - wx[i];
+        if (hu) {
+            T ax[9], bu[9];
+            const auto st = C.st(k);
+            opA(st + S::W, C.beta, wx, ax);
+            opB<T, ROBOT>(st, ou, bu);
+            for (int i = 0; i < 9; ++i) vb[(1 + k) * 9 + i] = r1[i] - (ax[i] + bu[i]);
+        }
+        wave_sync();
+        if (k >= 1)
+            for (int i = 0; i < 9; ++i) vb[k * 9 + i] += wx[i];
+    }
 }
 template <typename T, int ROBOT> __device__ __forceinline__ void phase_w(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu) {
     using S = Stage<ROBOT>;
@@ -1465,27 +1487,6 @@ template <typename T, int ROBOT> __device__ __forceinline__ void phase_w_pred(co
 }
 
 
-// (5b) Schur right-hand side blocks owned by knot k: rhs = r_e - E w, written into the LDS vector
-template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_rhs(const Ctx<T, ROBOT> &C, int k) {
-    using S = Stage<ROBOT>;
-    const int N = C.N;
-    T wx[9], wx1[9], wu[NU], r0[9], r1[9];
-    ldv(C.kv(WF(wx), k), wx);
-    ldv(C.kv(WF(wx), k < N ? k + 1 : k), wx1);
-    ldv(C.kv(WF(wu), k), wu);
-    ldv(C.bv(WF(rde), k == N ? N + 1 : 0), r0);   // boundary rows (k = 0: init, k = N: final)
-    ldv(C.bv(WF(rde), k < N ? 1 + k : 0), r1);     // dynamics rows of knot k
-    LdsT<T> *vb = C.vb;
-    if (k == 0) for (int i = 0; i < 9; ++i) vb[i] = r0[i] - wx[i];
-    if (k == N) for (int i = 0; i < 9; ++i) vb[(N + 1) * 9 + i] = r0[i] - wx[i];
-    if (k < N) {
-        T ax[9], bu[9];
-        const auto st = C.st(k);
-        opA(st + S::W, C.beta, wx, ax);
-        opB<T, ROBOT>(st, wu, bu);
-        for (int i = 0; i < 9; ++i) vb[(1 + k) * 9 + i] = r1[i] - (ax[i] + bu[i] - wx1[i]);
-    }
-}
 
 // (5d) direction at knot k from dnu; returns the max step allowed by this knot's rows
 // rows of knot k: ds = -r_i - G dz; dlambda from the push-through solves (TR, slack: dlt, dls;
@@ -1851,10 +1852,7 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
         }
         __syncthreads();
         STAMP(1);
-        for (int k = tid; k < K1; k += NT) {
-            phase_sblock<T, ROBOT>(C, k);
-            phase_rhs<T, ROBOT>(C, k);
-        }
+        for (int k = tid; k < K1; k += NT) phase_sblock<T, ROBOT>(C, k);
         __syncthreads();
         STAMP(2);
         // ---- factorization of S with the predictor's forward elimination fused in
@@ -1875,9 +1873,7 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
                 for (int k = tid; k < K1; k += NT) phase_w<T, ROBOT>(C, k, corr, sigma_mu);
                 __syncthreads();
                 STAMP(4);
-                for (int k = tid; k < K1; k += NT) phase_rhs<T, ROBOT>(C, k);
-                __syncthreads();
-                STAMP(5);
+                STAMP(5);   // (the right-hand side is formed inside phase_w)
                 tw_solve_elim<T>(C.So, NB, NBm, C.vb, ring);
                 __syncthreads();
                 if (tid < 64) tw_solve_meet<T>(C.Sd, C.So, NB, NBm, C.vb, shl);
