@@ -180,51 +180,6 @@ template <typename T, int ROBOT> struct Ctx {
         return (m >> ((row - R_::CP) / 4)) & 1u;
     }
     __device__ bool present(int k, int row) const { return present_m(cmask(k), row); }
-    // g'z - h of row `row` at knot k for the knot-local (x, t, u)
-    __device__ T gz(int k, int row, const T *x, T t, const T *u, bool with_h) const {
-        if (row < 8) {
-            T v = tr_sign<T>(row, 0) * x[6] + tr_sign<T>(row, 1) * x[7] + tr_sign<T>(row, 2) * x[8] + cw * t;
-            return with_h ? v - st(k)[S::BTR + row] : v;
-        }
-        if (row == 8) return -t;
-        if (row < R_::CP) {
-            const int c = (row - R_::FR) / 4, r = (row - R_::FR) % 4;
-            const auto cs = st(k) + (S::CON + S::CS * c);
-            const T *f = u + NUPC * c + FO;
-            T v = cs[S::G + 3 * r] * f[0] + cs[S::G + 3 * r + 1] * f[1] + cs[S::G + 3 * r + 2] * f[2];
-            return with_h ? v - cs[S::H + r] : v;
-        }
-        const int c = (row - R_::CP) / 4, dd = ((row - R_::CP) % 4) / 2, side = (row - R_::CP) % 2;
-        const T cop = u[NUPC * c + dd];
-        if (side == 0) {   // cop <= hi
-            return with_h ? cop - prm->foot_range[dd == 0 ? 0 : 2] : cop;
-        } else {           // -cop <= -lo, lo = -(lxn | lyn)
-            return with_h ? -cop - prm->foot_range[dd == 0 ? 1 : 3] : -cop;
-        }
-    }
-    // accumulate G' v of knot k into (gx (L part), gt, gu)
-    __device__ void gtv(int k, const T *v, T *gL, T &gt, T *gu) const {
-        gL[0] = gL[1] = gL[2] = T(0);
-        gt = T(0);
-        for (int j = 0; j < 8; ++j) {
-            for (int i = 0; i < 3; ++i) gL[i] += tr_sign<T>(j, i) * v[j];
-            gt += cw * v[j];
-        }
-        gt -= v[8];
-        if (k >= N) return;
-        for (int i = 0; i < NU; ++i) gu[i] = T(0);
-        for (int c = 0; c < NC; ++c) {   // rows of inactive contacts carry v = 0 and G = 0
-            const auto cs = st(k) + (S::CON + S::CS * c);
-            for (int r = 0; r < 4; ++r) {
-                const T vr = v[R_::FR + 4 * c + r];
-                for (int q = 0; q < 3; ++q) gu[NUPC * c + FO + q] += cs[S::G + 3 * r + q] * vr;
-            }
-            if (ROBOT == 1) {
-                for (int dd = 0; dd < 2; ++dd)
-                    gu[NUPC * c + dd] += v[R_::CP + 4 * c + 2 * dd] - v[R_::CP + 4 * c + 2 * dd + 1];
-            }
-        }
-    }
     __device__ SV<T> var_x(int k) const { return kv(Ws<ROBOT>::x, k); }
     __device__ SV<T> var_u(int k) const { return kv(Ws<ROBOT>::u, k); }
 };
@@ -237,18 +192,6 @@ __device__ __forceinline__ int pk9(int i, int j) { return i >= j ? i * (i + 1) /
 template <typename T> __device__ __forceinline__ T sym3(const T *p, int i, int j) {
     if (i < j) { int t = i; i = j; j = t; }
     return p[i * (i + 1) / 2 + j];
-}
-template <typename T> __device__ void inv3sym(const T (&a)[3][3], T *out) {
-    const T c00 = a[1][1] * a[2][2] - a[1][2] * a[2][1];
-    const T c01 = a[1][2] * a[2][0] - a[1][0] * a[2][2];
-    const T c02 = a[1][0] * a[2][1] - a[1][1] * a[2][0];
-    const T det = a[0][0] * c00 + a[0][1] * c01 + a[0][2] * c02;
-    const T id = T(1) / det;
-    const T c11 = a[0][0] * a[2][2] - a[0][2] * a[2][0];
-    const T c12 = a[0][2] * a[1][0] - a[0][0] * a[1][2];
-    const T c22 = a[0][0] * a[1][1] - a[0][1] * a[1][0];
-    out[0] = c00 * id; out[1] = c01 * id; out[2] = c11 * id;
-    out[3] = c02 * id; out[4] = c12 * id; out[5] = c22 * id;
 }
 // inverse of a 4x4 SPD matrix (Cholesky), packed symmetric (10 entries, row i col j<=i)
 template <typename T> __device__ void inv4spd(T (&a)[4][4], T *out) {
