@@ -188,6 +188,16 @@ template <typename T, int ROBOT> struct Ctx {
 // triangle, row-major: (i, j), j <= i at i (i + 1) / 2 + j; 45 of a block's 81 slots)
 __device__ __forceinline__ int pk9(int i, int j) { return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i; }
 
+// The coupling blocks S_{j,j+1} = -M A' (and the first / last, +M A' and -M) share the structure of
+// M A' = [[Mc, 0, Mc W'], [beta Ml, Ml, 0], [0, 0, M_LL]]: 27 structural nonzeros of 81, stored
+// compactly (row-major over the pattern) until the factorization overwrites the block with the
+// dense X_j / Y_j.  cp9(i, j): compact slot of (i, j), or -1 off the pattern.
+__device__ __forceinline__ int cp9(int i, int j) {
+    if (i < 3) return j == i ? 4 * i : (j >= 6 ? 4 * i + 1 + (j - 6) : -1);
+    if (i < 6) return j == i - 3 ? 12 + 2 * (i - 3) : (j == i ? 13 + 2 * (i - 3) : -1);
+    return j >= 6 ? 18 + 3 * (i - 6) + (j - 6) : -1;
+}
+
 // 3x3 symmetric packed (00,10,11,20,21,22) helpers
 template <typename T> __device__ __forceinline__ T sym3(const T *p, int i, int j) {
     if (i < j) { int t = i; i = j; j = t; }
@@ -690,7 +700,7 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_sblock(const C
         for (int i = 0; i < 9; ++i)
             for (int j = 0; j < 9; ++j) {
                 if (j <= i) Sd[pk9(i, j)] = Mfull(f0, i, j);
-                So[i * 9 + j] = MAt(f0, w, i, j);
+                if (cp9(i, j) >= 0) So[cp9(i, j)] = MAt(f0, w, i, j);   // compact coupling block
             }
     }
     if (k == N) {
@@ -754,14 +764,12 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_sblock(const C
     for (int i = 0; i < 9; ++i)
 #pragma unroll
         for (int j = 0; j <= i; ++j) Sd[i * (i + 1) / 2 + j] = Sm[i][j];
-    T *So = C.So + (size_t)(1 + k) * 81;
-    if (k + 1 < N) {
-        for (int i = 0; i < 9; ++i)
-            for (int j = 0; j < 9; ++j) So[i * 9 + j] = -MAt(f1, w1, i, j);
-    } else {
-        for (int i = 0; i < 9; ++i)
-            for (int j = 0; j < 9; ++j) So[i * 9 + j] = -Mfull(f1, i, j);
-    }
+    T *So = C.So + (size_t)(1 + k) * 81;   // compact coupling block (cp9)
+#pragma unroll
+    for (int i = 0; i < 9; ++i)
+#pragma unroll
+        for (int j = 0; j < 9; ++j)
+            if (cp9(i, j) >= 0) So[cp9(i, j)] = k + 1 < N ? -MAt(f1, w1, i, j) : -Mfull(f1, i, j);
 }
 
 // (4) two-ended ("twisted") block-Thomas factorization of the SPD block-tridiagonal S with
@@ -1060,14 +1068,18 @@ __device__ void tw_factor_ends(T *Sd, T *So, int NB, int m, LdsT<T> *sh, LdsT<T>
     LdsT<T> *A = sh + (top ? 0 : TW_SCRATCH), *P = A + 88, *Xb = A + 176, *Ob = A + 264, *Dd = A + 352,
             *Dn = A + 368;
     const int j0 = top ? 0 : NB - 1, dj = top ? 1 : -1, nstep = top ? m : NB - 1 - m;
-    int e[NE], et[NE], ep[NE];
+    int e[NE], et[NE], ep[NE], ec[NE];
     bool ok[NE];
+    T em[NE];
 #pragma unroll
     for (int q = 0; q < NE; ++q) {
         ok[q] = l + 32 * q < 81;
         e[q] = ok[q] ? l + 32 * q : 80;
         et[q] = top ? e[q] : (e[q] % 9) * 9 + e[q] / 9;   // landing slot of a coupling element
         ep[q] = pk9(e[q] / 9, e[q] % 9);                   // packed slot of a diagonal-block element
+        const int c = cp9(e[q] / 9, e[q] % 9);            // compact slot of a coupling element
+        ec[q] = c >= 0 ? c : 0;
+        em[q] = c >= 0 ? T(1) : T(0);                     // off-pattern elements land as zeros
     }
     unsigned long long sub[4] = {0, 0, 0, 0};
     unsigned long long *subp = (stamp_out && top) ? sub : nullptr;
@@ -1087,7 +1099,7 @@ __device__ void tw_factor_ends(T *Sd, T *So, int NB, int m, LdsT<T> *sh, LdsT<T>
         const T *On = So + (size_t)(top ? (jn > 0 ? jn - 1 : 0) : jn) * 81, *Dnx = Sd + (size_t)jn * 81;
         T pv[NE], nv[NE];
 #pragma unroll
-        for (int q = 0; q < NE; ++q) { pv[q] = On[e[q]]; nv[q] = Dnx[ep[q]]; }
+        for (int q = 0; q < NE; ++q) { pv[q] = On[ec[q]] * em[q]; nv[q] = Dnx[ep[q]]; }
         if (act) {
             if (s == 0)
                 tw_step_sym<T>(Dn, nullptr, nullptr, nullptr, Sd + (size_t)j * 81, A, P, Xb, Dd, vb, j, 0, subp);
@@ -1116,9 +1128,13 @@ template <typename T> __device__ void tw_factor_meet(T *Sd, T *So, int m, LdsT<T
     const bool has1 = e1 < 81;
     LdsT<T> *A = sh, *P = A + 88, *Xb = A + 176, *Op = A + 264, *Dd = A + 352;
     LdsT<T> *Pq = sh + TW_SCRATCH + 88, *Oq = sh + TW_SCRATCH + 264;
-    Op[e0] = So[(size_t)(m - 1) * 81 + e0];
-    Oq[e0] = So[(size_t)m * 81 + e0];
-    if (has1) { Op[e1] = So[(size_t)(m - 1) * 81 + e1]; Oq[e1] = So[(size_t)m * 81 + e1]; }
+    auto cpl = [&](const T *blk, int e) -> T {   // compact coupling block -> element e (zero off-pattern)
+        const int c = cp9(e / 9, e % 9);
+        return blk[c >= 0 ? c : 0] * (c >= 0 ? T(1) : T(0));
+    };
+    Op[e0] = cpl(So + (size_t)(m - 1) * 81, e0);
+    Oq[e0] = cpl(So + (size_t)m * 81, e0);
+    if (has1) { Op[e1] = cpl(So + (size_t)(m - 1) * 81, e1); Oq[e1] = cpl(So + (size_t)m * 81, e1); }
     LdsT<T> *Dn = A + 368;
     Dn[e0] = Sd[(size_t)m * 81 + pk9(e0 / 9, e0 % 9)];
     if (has1) Dn[e1] = Sd[(size_t)m * 81 + pk9(e1 / 9, e1 % 9)];
