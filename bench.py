@@ -29,6 +29,8 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, 'centroidal-mpc_amd')]
 import numpy as np  # noqa: E402
 
 METRIC = 'SCP iterations/sec, Solo12-trot N=100 batch=1024 @ 1/2/4/8 GPU'
+WORKLOAD_NAMES = {'trot': 'conf_solo12_trot', 'bound': 'conf_solo12_bound', 'pace': 'conf_solo12_pace',
+                  'talos': 'conf_talos', 'mixed': 'Solo12 pace+trot mixed contact plans'}
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
@@ -94,7 +96,10 @@ def main():
         import torch.distributed as dist  # gloo: barrier and timing reduction only (no data path)
         dist.init_process_group('gloo', rank=rank, world_size=world)
 
-    pb = make_batch(args.config, args.N, args.batch, seed_offset=rank * args.batch)
+    if args.config == 'mixed':     # BASELINE C5: pace and trot contact plans alternating in one batch
+        pb = make_batch('trot', args.N, args.batch, seed_offset=rank * args.batch, mixed=('pace', 'trot'))
+    else:
+        pb = make_batch(args.config, args.N, args.batch, seed_offset=rank * args.batch)
     solver = Solver(pb.robot, args.N, args.batch, args.precision, device=local_rank)
     solver.upload(pb)
     for _ in range(args.warmup):
@@ -129,7 +134,8 @@ def main():
     achieved = algorithmic_qp_bytes(args.N, ipm_total, w) / qp_mean_s / 1e9
     traffic = None
     pmc = os.path.join(ROOT, 'profiles', 'qp_pmc_traffic.json')
-    if os.path.exists(pmc):
+    metric_config = (args.config, args.N, args.batch, w) == ('trot', 100, 1024, 8)
+    if metric_config and os.path.exists(pmc):   # the PMC summary was measured on the metric config only
         try:
             traffic = json.load(open(pmc)).get('hbm_bytes_per_launch')
         except Exception:
@@ -147,8 +153,8 @@ def main():
         'vs_baseline': None,
         'dtype': 'f64' if w == 8 else 'f32',
         'data': 'synthetic (seeded contact plans + dynamically consistent warm starts, cmpc/synth.py)',
-        'config': {'workload': 'conf_solo12_trot SCP iterations (fixed-K), N=%d, %d problems per GPU'
-                               % (args.N, args.batch),
+        'config': {'workload': '%s SCP iterations (fixed-K), N=%d, %d problems per GPU'
+                               % (WORKLOAD_NAMES.get(args.config, args.config), args.N, args.batch),
                    'config': args.config, 'N': args.N, 'batch_per_gpu': args.batch,
                    'global_batch': args.batch * world, 'parallelism': 'batch-sharded x%d' % world},
         'phase_ms_per_step': {k: tim[k] / max(tim['iterations'], 1)
