@@ -230,3 +230,28 @@ def test_qp_horizon_edges(cfg, N, B):
         assert k['dual'] <= 1e-6 * scale, (k['dual'], scale)
         assert k['sign'] == 0.0
     s.close()
+
+
+@pytest.mark.parametrize('cfg,N,B,prec,mixed', [
+    ('bound', 100, 1024, 'fp32', None),          # BASELINE C3: fp32 + tolerance check vs CPU
+    ('talos', 200, 512, 'fp64', None),           # BASELINE C4: one GPU's shard of 4096
+    ('trot', 150, 1024, 'fp64', ('pace', 'trot')),  # BASELINE C5: one GPU's shard of 8192, mixed plans
+])
+def test_full_size_baseline_configs(cfg, N, B, prec, mixed):
+    """Full per-GPU sizes of BASELINE C3-C5: every QP solved; on a sample, KKT primal residual of
+    the reference-form QP (fp64 1e-8, fp32 1e-3) and |X| within 1e-5 (fp64) / 5e-3 (fp32) of the
+    oracle's independent sparse IPM on the same QP."""
+    pb, s = _solver(cfg, N, B, prec, mixed=mixed)
+    s.scp_iterate(fixed_iters=True)
+    z, y, st, it = s.qp_solution(with_y=True)
+    assert np.all(st == 1), np.unique(st, return_counts=True)
+    nx = 9 * (N + 1)
+    tol_prim, tol_x = (1e-3, 5e-3) if prec == 'fp32' else (1e-8, 1e-5)
+    for b in (0, B - 1):
+        P, q, A, l, u = s.export_qp(b)
+        k = kkt_residuals(P, q, A, l, u, z[b])
+        assert k['prim'] <= tol_prim, (b, k)
+        ref = sparse_ipm_qp(P, q, A, l, u)
+        err = np.abs(z[b][:nx] - ref.x[:nx]).max() / np.abs(ref.x[:nx]).max()
+        assert err <= tol_x, (b, err, int(it[b]))
+    s.close()
