@@ -255,3 +255,23 @@ def test_full_size_baseline_configs(cfg, N, B, prec, mixed):
         err = np.abs(z[b][:nx] - ref.x[:nx]).max() / np.abs(ref.x[:nx]).max()
         assert err <= tol_x, (b, err, int(it[b]))
     s.close()
+
+
+@pytest.mark.xfail(strict=True, reason='known IPM stall (DESIGN.md section 8 item 4): TALOS N=200 problem 280, '
+                                       'second SCP iteration, ends at the 60-iteration cap')
+def test_talos_shrunk_trust_region_qp_solves():
+    """TALOS N=200 x 512, second fixed-K SCP iteration (trust region shrunk by the first reject):
+    every QP must reach 'solved' and match the oracle's sparse IPM on the same exported QP."""
+    N, B = 200, 512
+    pb, s = _solver('talos', N, B)
+    s.scp_iterate(fixed_iters=True)
+    s.scp_iterate(fixed_iters=True)
+    z, y, st, it = s.qp_solution(with_y=True)
+    b = int(it.argmax())
+    P, q, A, l, u = s.export_qp(b)
+    ref = sparse_ipm_qp(P, q, A, l, u)
+    nx = 9 * (N + 1)
+    err = np.abs(z[b][:nx] - ref.x[:nx]).max() / np.abs(ref.x[:nx]).max()
+    s.close()
+    assert np.all(st == 1), (np.nonzero(st != 1)[0], int(it.max()))
+    assert err <= 1e-5, err
