@@ -6,16 +6,27 @@ QP -> trust-region accept/reject) for every problem resident on the GPU, in the 
 fixed-K mode (every problem iterates each step).  Inputs are uploaded
 to HBM before the timed region; nothing is copied in or out inside it.
 
-Multi-GPU (launched by torch.distributed.run): one process per GPU, each rank owns its own
-shard of 1024 problems (weak scaling, no collective in the data path); a gloo barrier brackets
-the timed region and the max time over ranks is reported.
+Multi-GPU: one process per GPU, either launched by torch.distributed.run (the driver) or spawned
+here by ``--gpus N`` (cmpc/shard.py spawn_local; the parent never touches the GPU).  Ranks talk
+only over RCCL through libcmpc's C ABI (no PyTorch): rank 0 broadcasts the parameter classes, an
+RCCL max-reduction is the barrier around the timed region and takes the max time over ranks, and
+the accepted solutions are gathered to rank 0 after it (timed separately: ``gather_ms``).
+``value`` is weak scaling (1024 problems per GPU, no data-path collective: the path shards into
+independent problems); ``strong_scaling`` times the same steps with the global batch fixed at
+1024 split over the GPUs.
 
 Extra fields ("Measurement"):
-  roofline      QP kernel: algorithmic bytes per launch (SURVEY.md 8d per-IPM-iteration figure
-                x IPM iterations actually run) / its mean duration from HIP events recorded
-                on the library's stream over the timed region.
-  cpu_baseline  the oracle (numpy/scipy restatement of the reference path, OSQP algorithm at
-                the reference's eps 1e-7 with polish) on a bounded sample, rank 0 at N = 1 only.
+  roofline      QP kernel: algorithmic bytes per launch (SURVEY.md 8d per-IPM-iteration figure,
+                priced with the robot's own per-knot sizes, x IPM iterations actually run) / its
+                mean duration from HIP events recorded on the library's stream over the timed
+                region; ``compulsory`` prices the kernel's own minimum traffic per Newton step.
+  early_exit    the reference's semantics (src/scp_solver.py:133-134): solve until every problem
+                has left the loop, then copy X, U, K, Sigma to the host; SCP iterations executed /
+                wall time.
+  qp_exit       QP exit-status histogram and refinement counts of the last timed step.
+  cpu_baseline  the oracle (numpy/scipy restatement of the reference path, OSQP algorithm at the
+                reference's eps 1e-7 with polish) on bounded samples, rank 0 at N = 1 only:
+                throughput over the box's CPU share, single-core latency and early exit.
 """
 import argparse
 import json
@@ -32,31 +43,90 @@ METRIC = 'SCP iterations/sec, Solo12-trot N=100 batch=1024 @ 1/2/4/8 GPU'
 WORKLOAD_NAMES = {'trot': 'conf_solo12_trot', 'bound': 'conf_solo12_bound', 'pace': 'conf_solo12_pace',
                   'talos': 'conf_talos', 'mixed': 'Solo12 pace+trot mixed contact plans'}
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+CPU_SHARE = 16          # host cores of one GPU's share on the box
 
 
-def algorithmic_qp_bytes(N, ipm_iters_total, w):
-    """per IPM iteration one factorization pass N*w*(Lf + 2*103 + n_k + m_k)
-    (Lf = 451, n_k = 22, m_k = 38) plus two Newton solves of ~N*w*1000 each."""
-    per_iter = N * w * (451 + 2 * 103 + 22 + 38) + 2 * N * w * 1000
-    return per_iter * ipm_iters_total
+def per_knot_sizes(robot):
+    """SURVEY.md 8d per-knot sizes: n_k = nx + nu + 1, m_k rows, stored A values, factor values."""
+    if robot == 'solo12':
+        return dict(n_k=22, m_k=38, a_k=103, L_f=451)
+    return dict(n_k=22, m_k=32, a_k=82, L_f=451)    # TALOS: 9 + 10 + 9 + 4 rows, 82 stored A values
 
 
-def cpu_baseline(N, seconds_target=12.0):
-    """Time the oracle SCP iteration on host cores (bounded sample)."""
+def algorithmic_qp_bytes(N, ipm_iters_total, w, robot='solo12'):
+    """per IPM iteration one factorization pass N*w*(L_f + 2*a_k + n_k + m_k) plus two
+    Newton solves of N*w*(L_f + 1.5*a_k + 6*m_k + 3*n_k) each (~N*w*1000 for Solo12)."""
+    s = per_knot_sizes(robot)
+    fact = s['L_f'] + 2 * s['a_k'] + s['n_k'] + s['m_k']
+    solve = s['L_f'] + 1.5 * s['a_k'] + 6 * s['m_k'] + 3 * s['n_k']
+    return N * w * (fact + 2 * solve) * ipm_iters_total
+
+
+def compulsory_qp_bytes(N, ipm_iters_total, w, robot='solo12'):
+    """The kernel's own minimum traffic per Newton step: the stage record read
+    once, the iterate (s, lambda, x, u, t, nu) read and written once, the Schur blocks written (S_jj
+    packed 45 + compact coupling 27) and read by the factorization, the factors (I_j packed 45, X_j
+    or Y_j 81) written once and read by the two solves."""
+    stage = 160 if robot == 'solo12' else 96
+    state = 2 * (2 * 25 + 9 + 12 + 1 + 9)
+    sblocks = 2 * (45 + 27)
+    factors = 3 * (45 + 81)
+    return N * w * (stage + state + sblocks + factors) * ipm_iters_total
+
+
+def cpu_info():
+    model = None
+    try:
+        for line in open('/proc/cpuinfo'):
+            if line.startswith('model name'):
+                model = line.split(':', 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count()
+    return dict(os_cpu_count=os.cpu_count(), affinity=affinity, model=model)
+
+
+def cpu_baseline(N):
+    """The oracle on the GPU box's host cores, bounded samples (~15-25 s in all):
+    throughput: 96 problems per worker x one SCP iteration, over the box's CPU share (16 workers;
+      os.cpu_count() reports the whole machine there, see cpu_info);
+    latency: one core, 6 problems x one SCP iteration (seconds per problem iteration);
+    early exit: the reference's loop (src/scp_solver.py:118-179, exits after the first accept) on
+      8 problems per worker."""
     import multiprocessing as mp
-    cores = max(1, min(16, os.cpu_count() or 1))   # the GPU box's CPU share is 16
-    n_prob = 96 * cores                              # ~10-20 s of oracle work on the box
     from cmpc.synth import make_batch
+    info = cpu_info()
+    cores = max(1, min(CPU_SHARE, info['affinity'] or 1))
+    n_prob = 96 * cores
     pb = make_batch('trot', N, n_prob, seed_offset=777)
     probs = [pb.oracle_problem(b) for b in range(n_prob)]
+    ctx = mp.get_context('fork')
     t0 = time.perf_counter()
-    with mp.get_context('fork').Pool(cores, initializer=_cpu_init) as pool:
+    with ctx.Pool(cores, initializer=_cpu_init) as pool:
         pool.map(_cpu_one_iteration, probs, chunksize=1)
     dt = time.perf_counter() - t0
+    _cpu_init()
+    t1 = time.perf_counter()
+    for p in probs[:6]:
+        _cpu_one_iteration(p)
+    lat = (time.perf_counter() - t1) / 6
+    ee = probs[:8 * cores]
+    t2 = time.perf_counter()
+    with ctx.Pool(cores, initializer=_cpu_init) as pool:
+        iters = pool.map(_cpu_early_exit, ee, chunksize=1)
+    dt_ee = time.perf_counter() - t2
     return dict(value=n_prob / dt, unit='SCP iterations/s', cores=cores, kind='port',
                 sample='%d synthetic Solo12-trot N=%d problems, one SCP iteration each (oracle: numpy '
                        'linearization + reference-order CSC assembly + OSQP-algorithm ADMM eps 1e-7 with '
-                       'polish), %d worker processes, %.1f s wall' % (n_prob, N, cores, dt))
+                       'polish), %d worker processes, %.1f s wall' % (n_prob, N, cores, dt),
+                host=info,
+                single_core_latency_s=lat,
+                early_exit=dict(value=sum(iters) / dt_ee, unit='SCP iterations/s', problems=len(ee),
+                                iterations=int(sum(iters)), seconds=dt_ee))
 
 
 def _cpu_init():
@@ -71,67 +141,87 @@ def _cpu_one_iteration(prob):
     return 0
 
 
+def _cpu_early_exit(prob):
+    from oracle import scp as S
+    log = []
+    S.solve_scp(prob, prob['scp_params'], log=log)
+    return len(log)
+
+
+def make_problems(cfg, N, B, seed_offset):
+    from cmpc.synth import make_batch
+    if cfg == 'mixed':     # BASELINE C5: pace and trot contact plans alternating in one batch
+        return make_batch('trot', N, B, seed_offset=seed_offset, mixed=('pace', 'trot'))
+    return make_batch(cfg, N, B, seed_offset=seed_offset)
+
+
+def timed_steps(solver, comm, steps):
+    """K fixed-K SCP iterations between two barriers; (max-over-ranks seconds, HIP-event phase
+    timings of this rank)."""
+    solver.synchronize()
+    if comm is not None:
+        comm.barrier()
+    solver.timing_begin()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        solver.scp_iterate(fixed_iters=True)
+    solver.synchronize()
+    elapsed = time.perf_counter() - t0
+    tim = solver.timing_end()
+    if comm is not None:
+        elapsed = float(comm.allreduce_max([elapsed])[0])
+    return elapsed, tim
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=2)
-    ap.add_argument('--batch', type=int, default=1024, help='problems per GPU')
+    ap.add_argument('--batch', type=int, default=1024, help='problems per GPU (weak scaling)')
+    ap.add_argument('--global-batch', type=int, default=1024, help='strong-scaling global batch')
     ap.add_argument('--N', type=int, default=100)
     ap.add_argument('--config', default='trot')
     ap.add_argument('--precision', default='fp64')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-extras', action='store_true', help='skip strong-scaling and early-exit legs')
     args = ap.parse_args()
 
-    rank = int(os.environ.get('RANK', 0))
-    world = int(os.environ.get('WORLD_SIZE', 1))
-    local_rank = int(os.environ.get('LOCAL_RANK', 0))
+    from cmpc.shard import RcclComm, shard_bounds, spawn_local, world_from_env
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        # no launcher: one process per GPU, started before anything touches the GPU
+        sys.exit(spawn_local(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
+    rank, world, local_rank, addr, port = world_from_env()
 
-    # the library is loaded before torch so the process has exactly one HIP runtime
     from cmpc._lib import Solver
-    from cmpc.synth import make_batch
 
-    dist = None
-    if world > 1:
-        import torch.distributed as dist  # gloo: barrier and timing reduction only (no data path)
-        dist.init_process_group('gloo', rank=rank, world_size=world)
-
-    if args.config == 'mixed':     # BASELINE C5: pace and trot contact plans alternating in one batch
-        pb = make_batch('trot', args.N, args.batch, seed_offset=rank * args.batch, mixed=('pace', 'trot'))
-    else:
-        pb = make_batch(args.config, args.N, args.batch, seed_offset=rank * args.batch)
+    pb = make_problems(args.config, args.N, args.batch, rank * args.batch)
     solver = Solver(pb.robot, args.N, args.batch, args.precision, device=local_rank)
-    solver.upload(pb)
+    comm = RcclComm(solver, rank, world, addr, port) if world > 1 else None
+    if comm is not None:
+        comm.bcast_params(pb.params if rank == 0 else None, capacity=len(pb.params))
+        solver.upload(pb, set_params=False)
+    else:
+        solver.upload(pb)
     for _ in range(args.warmup):
         solver.scp_iterate(fixed_iters=True)
-    solver.synchronize()
-
-    def barrier():
-        solver.synchronize()
-        if dist is not None:
-            dist.barrier()
-
-    barrier()
-    solver.timing_begin()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        solver.scp_iterate(fixed_iters=True)
-    solver.synchronize()
-    t1 = time.perf_counter()
-    tim = solver.timing_end()
-    barrier()
-    elapsed = t1 - t0
+    elapsed, tim = timed_steps(solver, comm, args.steps)
     ipm_total = solver.qp_iterations_total()        # IPM iterations of the last step, all problems
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    _, _, qst, _ = solver.qp_solution(with_y=False)
+    merit, nref = solver.qp_info()
+    gather_ms = None
+    if comm is not None:
+        comm.barrier()
+        tg = time.perf_counter()
+        comm.gather_solution(root=0)
+        gather_ms = float(comm.allreduce_max([time.perf_counter() - tg])[0]) * 1e3
     units = args.batch * world * args.steps
     value = units / elapsed
     w = 8 if args.precision in ('fp64', 'f64', 'float64') else 4
-    qp_mean_s = tim['qp_ms'] / 1e3 / max(tim['iterations'], 1)
-    achieved = algorithmic_qp_bytes(args.N, ipm_total, w) / qp_mean_s / 1e9
+    n_steps = max(tim['iterations'], 1)
+    qp_mean_s = tim['qp_ms'] / 1e3 / n_steps
+    achieved = algorithmic_qp_bytes(args.N, ipm_total, w, pb.robot) / qp_mean_s / 1e9
+    compulsory = compulsory_qp_bytes(args.N, ipm_total, w, pb.robot) / qp_mean_s / 1e9
     traffic = None
     pmc = os.path.join(ROOT, 'profiles', 'qp_pmc_traffic.json')
     metric_config = (args.config, args.N, args.batch, w) == ('trot', 100, 1024, 8)
@@ -140,6 +230,7 @@ def main():
             traffic = json.load(open(pmc)).get('hbm_bytes_per_launch')
         except Exception:
             traffic = None
+    u, c = np.unique(qst, return_counts=True)
     out = {
         'metric': METRIC,
         'value': value,
@@ -156,13 +247,55 @@ def main():
         'config': {'workload': '%s SCP iterations (fixed-K), N=%d, %d problems per GPU'
                                % (WORKLOAD_NAMES.get(args.config, args.config), args.N, args.batch),
                    'config': args.config, 'N': args.N, 'batch_per_gpu': args.batch,
-                   'global_batch': args.batch * world, 'parallelism': 'batch-sharded x%d' % world},
-        'phase_ms_per_step': {k: tim[k] / max(tim['iterations'], 1)
-                              for k in ('linearize_ms', 'assemble_ms', 'qp_ms', 'accept_ms')},
+                   'global_batch': args.batch * world, 'parallelism': 'batch-sharded x%d (RCCL)' % world},
+        'phase_ms_per_step': {k: tim[k] / n_steps for k in ('linearize_ms', 'assemble_ms', 'qp_ms', 'accept_ms')},
         'qp_ipm_iterations_mean': ipm_total / args.batch,
+        'qp_exit': {'status_counts': {str(int(a)): int(b) for a, b in zip(u, c)},
+                    'merit_max': float(merit.max()), 'refined_problems': int((nref > 0).sum()),
+                    'refine_steps': int(nref.sum())},
         'roofline': {'kernel': 'k_qp_ipm', 'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
-                     'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic},
+                     'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
+                     'compulsory': {'achieved': compulsory, 'frac': compulsory / HBM_PEAK_GBS}},
     }
+    if gather_ms is not None:
+        out['gather_ms'] = gather_ms
+    if not args.no_extras:
+        # strong scaling: the global batch fixed, contiguous slices over the ranks
+        if world > 1:
+            lo, hi = shard_bounds(args.global_batch, rank, world)
+            per = -(-args.global_batch // world)
+            pbs = make_problems(args.config, args.N, per, lo)
+            s2 = Solver(pbs.robot, args.N, per, args.precision, device=local_rank)
+            s2.upload(pbs)
+            for _ in range(args.warmup):
+                s2.scp_iterate(fixed_iters=True)
+            el2, _ = timed_steps(s2, comm, args.steps)
+            s2.close()
+            out['strong_scaling'] = {'global_batch': args.global_batch, 'per_gpu': per,
+                                     'value': args.global_batch * args.steps / el2,
+                                     'ms_per_step': el2 / args.steps * 1e3}
+        # early exit, the reference's loop semantics, device-resident inputs, outputs copied back
+        solver.upload(pb, set_params=comm is None)
+        solver.synchronize()
+        if comm is not None:
+            comm.barrier()
+        t0 = time.perf_counter()
+        n_loop = solver.solve_scp(fixed_iters=False)
+        sol = solver.solution()          # X, U, K, Sigma and statuses to the host
+        dt_ee = time.perf_counter() - t0
+        iters = int(sol['iterations'].sum())
+        if comm is not None:
+            v = np.zeros(world + 1)
+            v[0] = dt_ee
+            v[1 + rank] = iters
+            v = comm.allreduce_max(v)
+            dt_ee, iters_all = float(v[0]), int(v[1:].sum())
+        else:
+            iters_all = iters
+        out['early_exit'] = {'value': iters_all / dt_ee, 'unit': 'SCP iterations/s', 'ms': dt_ee * 1e3,
+                             'scp_iterations': iters_all, 'loop_launches': int(n_loop),
+                             'accepted': int((sol['n_accepted'] > 0).sum()),
+                             'note': 'solve_scp until every problem leaves the loop + D2H of X, U, K, Sigma'}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out['cpu_baseline'] = cpu_baseline(args.N)
@@ -170,9 +303,9 @@ def main():
             out['cpu_baseline'] = {'error': repr(e)}
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if comm is not None:
+        comm.close()
     solver.close()
-    if dist is not None:
-        dist.destroy_process_group()
 
 
 if __name__ == '__main__':

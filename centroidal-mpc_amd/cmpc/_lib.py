@@ -14,7 +14,8 @@ LIB_PATH = os.path.join(_HERE, 'libcmpc_diag.so' if os.environ.get('CMPC_LIB_VAR
 
 ROBOTS = {'solo12': 0, 'TALOS': 1}
 PREC = {'fp64': 0, 'float64': 0, 'f64': 0, 'fp32': 1, 'float32': 1, 'f32': 1}
-QP_STATUS = {1: 'solved', -2: 'maximum iterations reached', -3: 'primal infeasible', -10: 'non-finite'}
+QP_STATUS = {1: 'solved', 2: 'solved inaccurate', -2: 'maximum iterations reached', -3: 'primal infeasible',
+             -4: 'dual infeasible', -10: 'non-finite'}
 SCP_STATUS = {0: 'running', 1: 'converged', 2: 'max_iter', -1: 'qp_failed'}
 DECISION = {0: 'none', 1: 'accept', 2: 'reject_rho', 3: 'reject_tr', -1: 'qp_failed'}
 
@@ -61,7 +62,9 @@ EXPORTS = ['cmpc_create', 'cmpc_destroy', 'cmpc_last_error', 'cmpc_version', 'cm
            'cmpc_get_solution', 'cmpc_get_iteration_log', 'cmpc_get_timing', 'cmpc_timing_begin',
            'cmpc_timing_end', 'cmpc_get_qp_iterations_total', 'cmpc_debug_stamps', 'cmpc_set_scp_mode',
            'cmpc_get_linearization_point', 'cmpc_interpolate', 'cmpc_generate_contact_plans',
-           'cmpc_upload_states', 'cmpc_get_contact_plans', 'cmpc_get_warm_start']
+           'cmpc_upload_states', 'cmpc_get_contact_plans', 'cmpc_get_warm_start', 'cmpc_get_qp_info',
+           'cmpc_comm_get_unique_id', 'cmpc_comm_init', 'cmpc_comm_destroy', 'cmpc_comm_bcast_params',
+           'cmpc_comm_allreduce_max', 'cmpc_comm_gather_solution']
 SCP_MODE = {'reference': 0, 'gusto': 1}
 
 _lib = None
@@ -116,6 +119,13 @@ def load():
         'cmpc_upload_states': (i32, [h, i32, vp, vp, vp]),
         'cmpc_get_contact_plans': (i32, [h, vp, vp, vp]),
         'cmpc_get_warm_start': (i32, [h, vp, vp]),
+        'cmpc_get_qp_info': (i32, [h, vp, vp]),
+        'cmpc_comm_get_unique_id': (i32, [vp]),
+        'cmpc_comm_init': (i32, [h, i32, i32, vp]),
+        'cmpc_comm_destroy': (i32, [h]),
+        'cmpc_comm_bcast_params': (i32, [h, i32, i32, P(Params)]),
+        'cmpc_comm_allreduce_max': (i32, [h, vp, i32]),
+        'cmpc_comm_gather_solution': (i32, [h, i32, vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -212,12 +222,14 @@ class Solver:
         arr = (Params * len(params))(*[params_struct(p, self.nc) for p in params])
         self._chk(self.lib.cmpc_set_params(self.h, len(params), arr), 'cmpc_set_params')
 
-    def upload(self, pb):
-        """ProblemBatch -> device (resets the SCP state of every problem)."""
+    def upload(self, pb, set_params=True):
+        """ProblemBatch -> device (resets the SCP state of every problem).  ``set_params=False``
+        keeps the installed parameter classes (e.g. broadcast from rank 0 by RCCL)."""
         if pb.robot != self.robot or pb.N != self.N:
             raise CmpcError('batch robot/N (%s, %d) does not match the handle (%s, %d)'
                             % (pb.robot, pb.N, self.robot, self.N))
-        self.set_params(pb.params)
+        if set_params:
+            self.set_params(pb.params)
         self._keep = [np.ascontiguousarray(pb.class_id, np.int32), np.ascontiguousarray(pb.logic, np.int8),
                       np.ascontiguousarray(pb.pos, float), np.ascontiguousarray(pb.rot, float),
                       np.ascontiguousarray(pb.Xbar, float), np.ascontiguousarray(pb.Ubar, float)]
@@ -345,6 +357,13 @@ class Solver:
         st = np.zeros(self.B, np.int32); it = np.zeros(self.B, np.int32)
         self._chk(self.lib.cmpc_get_qp_solution(self.h, _ptr(z), _ptr(y), _ptr(st), _ptr(it)), 'cmpc_get_qp_solution')
         return z, y, st, it
+
+    def qp_info(self):
+        """Per-problem exit data of the last QP solve: final merit (<= 1 when solved) and the number of
+        iterative-refinement steps taken."""
+        merit = np.zeros(self.B); nref = np.zeros(self.B, np.int32)
+        self._chk(self.lib.cmpc_get_qp_info(self.h, _ptr(merit), _ptr(nref)), 'cmpc_get_qp_info')
+        return merit, nref
 
     def solution(self):
         B, N = self.B, self.N

@@ -13,6 +13,7 @@
 
 #include "cmpc.h"
 #include "common.hpp"
+#include "handle.hpp"
 
 namespace cmpc {
 template <typename T, int R> __global__ void k_linearize(DevBuf<T>, int);
@@ -28,19 +29,9 @@ size_t ipm_workspace_elems(int N, int robot);
 }  // namespace cmpc
 
 using namespace cmpc;
+using namespace cmpc_host;
 
 namespace {
-
-struct Fail {
-    int code;
-    std::string msg;
-};
-
-#define HIPCHK(x)                                                                                   \
-    do {                                                                                            \
-        hipError_t e_ = (x);                                                                        \
-        if (e_ != hipSuccess) throw Fail{-3, std::string(#x) + ": " + hipGetErrorString(e_)};      \
-    } while (0)
 
 // Inverse standard normal CDF (Acklam's rational approximation refined by Halley steps on
 // erfc), to reproduce scipy.stats.norm.ppf for xi (reference src/constraints.py:157).
@@ -78,108 +69,7 @@ double norm_ppf(double p) {
 
 }  // namespace
 
-struct cmpc_handle_s {
-    int device = 0, robot = 0, N = 0, max_batch = 0, prec = 0, B = 0, n_classes = 0;
-    int NC = 4, NI = 25, SS = 160;
-    hipStream_t stream = nullptr;
-    hipEvent_t ev[5] = {};
-    bool timed = false;
-    // accumulated timing: one 5-event record per cmpc_scp_iterate since cmpc_timing_reset
-    std::vector<std::array<hipEvent_t, 5>> ev_pool;
-    size_t ev_used = 0;
-    bool accumulate = false;
-    std::string err;
-    cmpc_qp_settings qs{};
-    std::vector<cmpc_params> hparams;
-    std::vector<void *> allocs;
-    size_t ws_stride = 0;
-    // device pointers (typed by precision at use)
-    void *class_id = nullptr, *params = nullptr, *logic = nullptr, *pos = nullptr, *rot = nullptr, *Xbar = nullptr,
-         *Ubar = nullptr, *f = nullptr, *A = nullptr, *Bu = nullptr, *C = nullptr, *K = nullptr, *Sig = nullptr,
-         *Acl = nullptr, *Qw = nullptr, *stage = nullptr, *cw = nullptr, *xs = nullptr, *us = nullptr, *ts = nullptr,
-         *nus = nullptr, *lams = nullptr, *qp_status = nullptr, *qp_iters = nullptr, *ws = nullptr, *scp = nullptr,
-         *Xacc = nullptr, *Uacc = nullptr, *Kacc = nullptr, *Sacc = nullptr, *stamps = nullptr, *Xlin = nullptr,
-         *Ulin = nullptr;
-    int scp_mode = CMPC_SCP_MODE_REFERENCE;
-    int plans_B = 0;   // problems whose contact plans were built on the device
-
-    size_t esz() const { return prec == CMPC_PREC_F64 ? 8 : 4; }
-    void *dalloc(size_t bytes) {
-        void *p = nullptr;
-        HIPCHK(hipMalloc(&p, std::max<size_t>(bytes, 16)));
-        HIPCHK(hipMemsetAsync(p, 0, std::max<size_t>(bytes, 16), stream));
-        allocs.push_back(p);
-        return p;
-    }
-    template <typename T> DevBuf<T> buf() const {
-        DevBuf<T> d;
-        d.B = B; d.N = N;
-        d.class_id = (const int32_t *)class_id; d.params = (const DevParams<T> *)params;
-        d.logic = (const uint8_t *)logic; d.pos = (const T *)pos; d.rot = (const T *)rot;
-        d.Xbar = (const T *)Xbar; d.Ubar = (const T *)Ubar;
-        d.Xlin = (T *)Xlin; d.Ulin = (T *)Ulin; d.scp_mode = scp_mode;
-        d.f = (T *)f; d.A = (T *)A; d.Bu = (T *)Bu; d.C = (T *)C; d.K = (T *)K; d.Sig = (T *)Sig;
-        d.Acl = (T *)Acl; d.Qw = (T *)Qw; d.stage = (T *)stage; d.cw = (T *)cw;
-        d.xs = (T *)xs; d.us = (T *)us; d.ts = (T *)ts; d.nus = (T *)nus; d.lams = (T *)lams;
-        d.qp_status = (int32_t *)qp_status; d.qp_iters = (int32_t *)qp_iters;
-        d.ws = (T *)ws; d.ws_stride = ws_stride; d.scp = (ScpState *)scp;
-        d.Xacc = (T *)Xacc; d.Uacc = (T *)Uacc; d.Kacc = (T *)Kacc; d.Sacc = (T *)Sacc;
-        d.stamps = (unsigned long long *)stamps;
-        return d;
-    }
-};
-
 namespace {
-
-template <typename F> int guard(cmpc_handle h, F &&fn) {
-    try {
-        if (!h) return -1;
-        HIPCHK(hipSetDevice(h->device));
-        fn();
-        h->err.clear();
-        return 0;
-    } catch (const Fail &f) {
-        if (h) h->err = f.msg;
-        return f.code;
-    } catch (const std::exception &e) {
-        if (h) h->err = e.what();
-        return -9;
-    }
-}
-
-void need(bool ok, const std::string &msg) {
-    if (!ok) throw Fail{-2, msg};
-}
-
-template <typename T> void to_dev(cmpc_handle h, void *dst, const double *src, size_t n) {
-    if (sizeof(T) == 8) {
-        HIPCHK(hipMemcpyAsync(dst, src, n * 8, hipMemcpyHostToDevice, h->stream));
-        HIPCHK(hipStreamSynchronize(h->stream));
-    } else {
-        std::vector<T> tmp(n);
-        for (size_t i = 0; i < n; ++i) tmp[i] = T(src[i]);
-        HIPCHK(hipMemcpyAsync(dst, tmp.data(), n * sizeof(T), hipMemcpyHostToDevice, h->stream));
-        HIPCHK(hipStreamSynchronize(h->stream));
-    }
-}
-
-template <typename T> void from_dev(cmpc_handle h, double *dst, const void *src, size_t n) {
-    if (!dst) return;
-    if (sizeof(T) == 8) {
-        HIPCHK(hipMemcpyAsync(dst, src, n * 8, hipMemcpyDeviceToHost, h->stream));
-        HIPCHK(hipStreamSynchronize(h->stream));
-    } else {
-        std::vector<T> tmp(n);
-        HIPCHK(hipMemcpyAsync(tmp.data(), src, n * sizeof(T), hipMemcpyDeviceToHost, h->stream));
-        HIPCHK(hipStreamSynchronize(h->stream));
-        for (size_t i = 0; i < n; ++i) dst[i] = double(tmp[i]);
-    }
-}
-
-void from_dev_raw(cmpc_handle h, void *dst, const void *src, size_t bytes) {
-    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
-}
 
 template <typename T> DevParams<T> conv_params(const cmpc_params &p, int nw) {
     DevParams<T> d{};
@@ -333,8 +223,8 @@ const char *cmpc_last_error(cmpc_handle h) { return h ? h->err.c_str() : "null h
 int cmpc_default_qp_settings(int precision, cmpc_qp_settings *s) {
     if (!s) return -1;
     s->max_iter = precision == CMPC_PREC_F64 ? 60 : 40;
-    s->eps_abs = precision == CMPC_PREC_F64 ? 1e-11 : 1e-6;
-    s->eps_rel = precision == CMPC_PREC_F64 ? 1e-11 : 1e-6;
+    s->eps_abs = precision == CMPC_PREC_F64 ? 1e-10 : 1e-6;
+    s->eps_rel = precision == CMPC_PREC_F64 ? 1e-10 : 1e-6;
     s->step_fraction = 0.99;
     return 0;
 }
@@ -384,6 +274,8 @@ int cmpc_create(cmpc_handle *out, int device, int robot, int N, int max_batch, i
         h->lams = h->dalloc(Bm * K1 * h->NI * e);
         h->qp_status = h->dalloc(Bm * 4);
         h->qp_iters = h->dalloc(Bm * 4);
+        h->qp_merit = h->dalloc(Bm * e);
+        h->qp_nref = h->dalloc(Bm * 4);
         h->ws_stride = ipm_workspace_elems(N, robot);
         h->ws = h->dalloc(Bm * h->ws_stride * e);
         h->scp = h->dalloc(Bm * sizeof(ScpState));
@@ -407,6 +299,7 @@ int cmpc_destroy(cmpc_handle h) {
     if (!h) return 0;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->comm && h->comm_free) h->comm_free(h->comm);
     for (void *p : h->allocs) (void)hipFree(p);
     for (auto &e : h->ev)
         if (e) (void)hipEventDestroy(e);
@@ -848,6 +741,15 @@ int cmpc_get_qp_solution(cmpc_handle h, double *z, double *y, int32_t *status, i
         }
         if (status) from_dev_raw(h, status, h->qp_status, (size_t)B * 4);
         if (iters) from_dev_raw(h, iters, h->qp_iters, (size_t)B * 4);
+    });
+}
+
+int cmpc_get_qp_info(cmpc_handle h, double *merit, int32_t *n_refine) {
+    return guard(h, [&] {
+        need(h->B > 0, "no problems uploaded");
+        if (h->prec == CMPC_PREC_F64) from_dev<double>(h, merit, h->qp_merit, h->B);
+        else from_dev<float>(h, merit, h->qp_merit, h->B);
+        if (n_refine) from_dev_raw(h, n_refine, h->qp_nref, (size_t)h->B * 4);
     });
 }
 

@@ -80,6 +80,8 @@ template <typename T> struct DevBuf {
     T *nus;                         // (B,N+2,9)
     T *lams;                        // (B,N+1,NI)
     int32_t *qp_status, *qp_iters;
+    T *qp_merit;                    // (B) final merit (residual / tolerance; <= 1 when solved)
+    int32_t *qp_nref;               // (B) refinement steps taken
     // IPM workspace
     T *ws;
     size_t ws_stride;               // elements per problem

@@ -1,0 +1,138 @@
+// Host-side state of a libcmpc handle and the helpers shared by the C ABI translation units
+// (cmpc_api.cpp: lifecycle, kernels, export; comm.cpp: RCCL batch split).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <string>
+#include <vector>
+
+#include "cmpc.h"
+#include "common.hpp"
+
+namespace cmpc_host {
+
+struct Fail {
+    int code;
+    std::string msg;
+};
+
+}  // namespace cmpc_host
+
+#define HIPCHK(x)                                                                                   \
+    do {                                                                                            \
+        hipError_t e_ = (x);                                                                        \
+        if (e_ != hipSuccess) throw cmpc_host::Fail{-3, std::string(#x) + ": " + hipGetErrorString(e_)}; \
+    } while (0)
+
+struct cmpc_handle_s {
+    int device = 0, robot = 0, N = 0, max_batch = 0, prec = 0, B = 0, n_classes = 0;
+    int NC = 4, NI = 25, SS = 160;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[5] = {};
+    bool timed = false;
+    // accumulated timing: one 5-event record per cmpc_scp_iterate since cmpc_timing_reset
+    std::vector<std::array<hipEvent_t, 5>> ev_pool;
+    size_t ev_used = 0;
+    bool accumulate = false;
+    std::string err;
+    cmpc_qp_settings qs{};
+    std::vector<cmpc_params> hparams;
+    std::vector<void *> allocs;
+    size_t ws_stride = 0;
+    // device pointers (typed by precision at use)
+    void *class_id = nullptr, *params = nullptr, *logic = nullptr, *pos = nullptr, *rot = nullptr, *Xbar = nullptr,
+         *Ubar = nullptr, *f = nullptr, *A = nullptr, *Bu = nullptr, *C = nullptr, *K = nullptr, *Sig = nullptr,
+         *Acl = nullptr, *Qw = nullptr, *stage = nullptr, *cw = nullptr, *xs = nullptr, *us = nullptr, *ts = nullptr,
+         *nus = nullptr, *lams = nullptr, *qp_status = nullptr, *qp_iters = nullptr, *qp_merit = nullptr,
+         *qp_nref = nullptr, *ws = nullptr, *scp = nullptr,
+         *Xacc = nullptr, *Uacc = nullptr, *Kacc = nullptr, *Sacc = nullptr, *stamps = nullptr, *Xlin = nullptr,
+         *Ulin = nullptr;
+    int scp_mode = CMPC_SCP_MODE_REFERENCE;
+    // RCCL communicator of the batch split (comm.cpp); nullptr until cmpc_comm_init
+    void *comm = nullptr;
+    int comm_rank = 0, comm_size = 1;
+    void (*comm_free)(void *) = nullptr;   // set by cmpc_comm_init, called by cmpc_destroy
+    int plans_B = 0;   // problems whose contact plans were built on the device
+
+    size_t esz() const { return prec == CMPC_PREC_F64 ? 8 : 4; }
+    void *dalloc(size_t bytes) {
+        void *p = nullptr;
+        HIPCHK(hipMalloc(&p, std::max<size_t>(bytes, 16)));
+        HIPCHK(hipMemsetAsync(p, 0, std::max<size_t>(bytes, 16), stream));
+        allocs.push_back(p);
+        return p;
+    }
+    template <typename T> cmpc::DevBuf<T> buf() const {
+        cmpc::DevBuf<T> d;
+        d.B = B; d.N = N;
+        d.class_id = (const int32_t *)class_id; d.params = (const cmpc::DevParams<T> *)params;
+        d.logic = (const uint8_t *)logic; d.pos = (const T *)pos; d.rot = (const T *)rot;
+        d.Xbar = (const T *)Xbar; d.Ubar = (const T *)Ubar;
+        d.Xlin = (T *)Xlin; d.Ulin = (T *)Ulin; d.scp_mode = scp_mode;
+        d.f = (T *)f; d.A = (T *)A; d.Bu = (T *)Bu; d.C = (T *)C; d.K = (T *)K; d.Sig = (T *)Sig;
+        d.Acl = (T *)Acl; d.Qw = (T *)Qw; d.stage = (T *)stage; d.cw = (T *)cw;
+        d.xs = (T *)xs; d.us = (T *)us; d.ts = (T *)ts; d.nus = (T *)nus; d.lams = (T *)lams;
+        d.qp_status = (int32_t *)qp_status; d.qp_iters = (int32_t *)qp_iters;
+        d.qp_merit = (T *)qp_merit; d.qp_nref = (int32_t *)qp_nref;
+        d.ws = (T *)ws; d.ws_stride = ws_stride; d.scp = (cmpc::ScpState *)scp;
+        d.Xacc = (T *)Xacc; d.Uacc = (T *)Uacc; d.Kacc = (T *)Kacc; d.Sacc = (T *)Sacc;
+        d.stamps = (unsigned long long *)stamps;
+        return d;
+    }
+};
+
+namespace cmpc_host {
+
+template <typename F> inline int guard(cmpc_handle h, F &&fn) {
+    try {
+        if (!h) return -1;
+        HIPCHK(hipSetDevice(h->device));
+        fn();
+        h->err.clear();
+        return 0;
+    } catch (const Fail &f) {
+        if (h) h->err = f.msg;
+        return f.code;
+    } catch (const std::exception &e) {
+        if (h) h->err = e.what();
+        return -9;
+    }
+}
+
+inline void need(bool ok, const std::string &msg) {
+    if (!ok) throw Fail{-2, msg};
+}
+
+template <typename T> inline void to_dev(cmpc_handle h, void *dst, const double *src, size_t n) {
+    if (sizeof(T) == 8) {
+        HIPCHK(hipMemcpyAsync(dst, src, n * 8, hipMemcpyHostToDevice, h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+    } else {
+        std::vector<T> tmp(n);
+        for (size_t i = 0; i < n; ++i) tmp[i] = T(src[i]);
+        HIPCHK(hipMemcpyAsync(dst, tmp.data(), n * sizeof(T), hipMemcpyHostToDevice, h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+    }
+}
+
+template <typename T> inline void from_dev(cmpc_handle h, double *dst, const void *src, size_t n) {
+    if (!dst) return;
+    if (sizeof(T) == 8) {
+        HIPCHK(hipMemcpyAsync(dst, src, n * 8, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+    } else {
+        std::vector<T> tmp(n);
+        HIPCHK(hipMemcpyAsync(tmp.data(), src, n * sizeof(T), hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+        for (size_t i = 0; i < n; ++i) dst[i] = double(tmp[i]);
+    }
+}
+
+inline void from_dev_raw(cmpc_handle h, void *dst, const void *src, size_t bytes) {
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+}
+
+}  // namespace cmpc_host

@@ -51,7 +51,7 @@ template <int ROBOT> struct Ws {
         s = 0, l = s + NI, x = l + NI, u = x + 9, t = u + NU, nu = t + 1, rdx = nu + 9, rdt = rdx + 9,
         rdu = rdt + 1, rde = rdu + NU, rdi = rde + 9, facx = rdi + NI, facu = facx + FX, wx = facu + NC * FU,
         wt = wx + 9, wu = wt + 1, dx = wu + NU, dt = dx + 9, du = dt + 1, ds = du + NU, dl = ds + NI,
-        dsa = dl + NI, dla = dsa + NI, rh = dla + NI, NF = rh + NI
+        dsa = dl + NI, dla = dsa + NI, rh = dla + NI, dn0 = rh + NI, NF = dn0 + 9
     };
     // Schur blocks (block-major 9x9): S_jj -> I_j, and S_{j,j+1} -> X_{j+1} / Y_j (tw_factor_ends)
     static constexpr size_t Sd = (size_t)NF * KPC, So = Sd + (size_t)NBMAX * 81;
@@ -236,6 +236,14 @@ template <typename T> __device__ void inv4spd(T (&a)[4][4], T *out) {
 }
 __device__ __forceinline__ int p4(int i, int j) { if (i < j) { int t = i; i = j; j = t; } return i * (i + 1) / 2 + j; }
 
+// iterative refinement of the corrector direction when its step length falls below
+// QP_REFINE_ALPHA, or mu failed to halve in the previous iteration, while the merit is already
+// below QP_REFINE_MERIT (late in the solve)
+#define QP_REFINE_ALPHA 0.5
+#define QP_REFINE_MERIT 1e6
+// relative threshold of the primal-infeasibility certificate (OSQP's eps_prim_inf analogue)
+#define QP_EPS_PINF 1e-6
+
 // relative floor on D^-1 in the push-through blocks (K = D^-1 + G W^-1 G')
 template <typename T> constexpr double KFLOOR = sizeof(T) == 8 ? 1e-12 : 1e-6;
 
@@ -361,6 +369,8 @@ __device__ __forceinline__ void contact_wd(const Ctx<T, ROBOT> &C, int c, bool a
 
 // ------------------------------------------------------------------ phases
 // (1) residuals of knot k; returns norm contributions
+// prim / dual / comp: residual maxima; mu: complementarity sum over cnt rows; sp / sd: scales of
+// the relative tolerances
 template <typename T, int ROBOT> struct Norms { T prim, dual, comp, mu, sp, sd, lmax, cnt; };
 
 // Per-knot phases follow load -> compute -> store: every store into the workspace comes after
@@ -521,6 +531,51 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_residual(const
     resid_knot<T, ROBOT>(C, k, nm, C.stage + k, ws + WF(x) * KPC + k, ws + WF(u) * KPC + k, ws + WF(t) * KPC + k,
                          ws + WF(s) * KPC + k, ws + WF(l) * KPC + k, ws + WF(nu) * KPC + k, ws + WF(rdx) * KPC + k,
                          ws + WF(rdt) * KPC + k, ws + WF(rdu) * KPC + k, ws + WF(rde) * KPC, ws + WF(rdi) * KPC + k);
+}
+
+// (1b) primal-infeasibility certificate terms of knot k (rare; after the residual phase):
+// cm[0] = max |E'nu + G'lambda| = |r_d - H z - q| over the knot's x, t, u entries, cm[1] = max |nu|
+// (lambda's max comes from the residual phase), cs += b'nu + h'lambda over the rows the knot owns
+template <typename T, int ROBOT>
+__device__ PHASE_ATTR void phase_cert(const Ctx<T, ROBOT> &C, int k, T (&cm)[2], T &cs) {
+    using S = Stage<ROBOT>;
+    using R_ = Rows<ROBOT>;
+    constexpr int NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC;
+    const int N = C.N;
+    const bool hu = k < N;
+    const SV<const T> st = C.st(hu ? k : 0);
+    const unsigned msk = C.cmask(k);
+    const SV<T> x = C.var_x(k), rdx = C.kv(WF(rdx), k), lm = C.kv(WF(l), k), nk = C.bv(WF(nu), k),
+                n1 = C.bv(WF(nu), k + 1);
+    for (int i = 0; i < 9; ++i) {
+        cm[0] = fmax(cm[0], fabs(rdx[i] - C.Wx(i) * x[i] - C.st(k)[S::QX + i]));
+        cm[1] = fmax(cm[1], fabs(nk[i]));
+        if (k == N) cm[1] = fmax(cm[1], fabs(n1[i]));
+    }
+    cm[0] = fmax(cm[0], fabs(C.kv(WF(rdt), k)[0] - T(1)));
+    if (hu) {
+        const SV<T> u = C.var_u(k), rdu = C.kv(WF(rdu), k);
+        for (int i = 0; i < NU; ++i) cm[0] = fmax(cm[0], fabs(rdu[i] - C.Wu(i) * u[i]));
+        for (int i = 0; i < 9; ++i) cs = fma(st[S::R + i], n1[i], cs);
+    }
+    if (k == 0 || k == N) {
+        const T *xb = C.xbar + (size_t)k * 9;
+        for (int i = 0; i < 9; ++i) cs = fma(xb[i], k == 0 ? nk[i] : n1[i], cs);
+    }
+    const SV<const T> sk = C.st(k);
+    for (int j = 0; j < 8; ++j) cs = fma(sk[S::BTR + j], lm[j], cs);   // slack rows: h = 0
+    if (!hu) return;
+    for (int c = 0; c < NC; ++c) {
+        if (!((msk >> c) & 1u)) continue;
+        const auto cs_ = st + (S::CON + S::CS * c);
+        for (int r = 0; r < 4; ++r) cs = fma(cs_[S::H + r], lm[R_::FR + 4 * c + r], cs);
+        if (ROBOT == 1)
+            for (int q = 0; q < 4; ++q) {   // cop <= hi | -cop <= -lo: h = hi | lxn, lyn
+                const int dd = q / 2;
+                cs = fma(C.prm->foot_range[dd == 0 ? (q % 2) : 2 + (q % 2)], lm[R_::CP + 4 * c + q], cs);
+            }
+    }
+    (void)NUPC;
 }
 
 // (2) Phi factors of knot k
@@ -1308,7 +1363,9 @@ __device__ void tw_solve_back(const T *Xs, int NB, int m, LdsT<T> *vb, LdsT<T> *
     wave_sync();
 }
 
-// r_hat = r_i - r_c / lambda for the rows of knot k  (rc supplied per mode)
+// r_hat = r_i - r_c / lambda for the rows of knot k.  corr 0 (predictor): r_c = s lambda; 1
+// (corrector): r_c = s lambda + ds_aff dlambda_aff - sigma mu; 2 (refinement): r_c = the dsa
+// field, which then holds the complementarity residual of the corrector direction (phase_lres)
 template <typename T, int ROBOT>
 __device__ __forceinline__ void rhat_rows(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu, const T *s, const T *lm,
                                           T *rh) {
@@ -1323,13 +1380,13 @@ __device__ __forceinline__ void rhat_rows(const Ctx<T, ROBOT> &C, int k, int cor
         T a[NI];
         ldv(C.kv(WF(dsa), k), a);
 #pragma unroll
-        for (int r = 0; r < NI; ++r) cc[r] = a[r] - sigma_mu;
+        for (int r = 0; r < NI; ++r) cc[r] = corr == 2 ? a[r] : a[r] - sigma_mu;
     }
 #pragma unroll
     for (int r = 0; r < NI; ++r) {
         const bool pr = Ctx<T, ROBOT>::present_m(msk, r);
         const T sr = s[r], lr = lm[r];
-        const T rc = sr * lr + cc[r];
+        const T rc = (corr == 2 ? T(0) : sr * lr) + cc[r];
         const T v = rd[r] - fdiv(rc, pr ? lr : T(1));
         rh[r] = pr ? v : T(0);
     }
@@ -1455,7 +1512,9 @@ template <typename T, int ROBOT> __device__ __forceinline__ void phase_w_pred(co
 // contact-by-contact streaming: each row's step is stored as soon as it is formed, so the knot
 // is never held in registers whole.  Inactive contacts: G = Gw = 0, Kinv = I, rhat = 0 -> zero
 // steps.
-template <typename T, int ROBOT>
+// ACC (refinement): the solve gives the correction of the corrector direction; the stored
+// direction becomes direction + correction and the ratio test runs on the sum.
+template <typename T, int ROBOT, bool ACC = false>
 __device__ __forceinline__ T dz_knot(const Ctx<T, ROBOT> &C, int k, T (&mus)[3], bool prod, const T *__restrict__ stp,
                                      const T *__restrict__ rhp, const T *__restrict__ rdxp, const T *__restrict__ rdtp,
                                      const T *__restrict__ wup, const T *__restrict__ ss, const T *__restrict__ ls,
@@ -1484,7 +1543,8 @@ __device__ __forceinline__ T dz_knot(const Ctx<T, ROBOT> &C, int k, T (&mus)[3],
     // stores: corrector ds, dl; predictor ds_aff dl_aff in the ds field (the corrector's r_hat
     // term) or, in the initialization step (whose full step is the affine one), ds_aff itself
     auto emit = [&](int r, bool pr, T g, T dlr, T sr, T lr, T rdir) {
-        const T dsr = pr ? -rdir - g : T(0);
+        T dsr = pr ? -rdir - g : T(0);
+        if (ACC) { dsr += ds[r * ld]; dlr += dl[r * ld]; }
         ds[r * ld] = prod ? dsr * dlr : dsr;
         dl[r * ld] = dlr;
         // sum_r (s + a ds)(lambda + a dl) = mus0 + a mus1 + a^2 mus2 (absent rows: lambda = ds = dl = 0)
@@ -1520,9 +1580,10 @@ __device__ __forceinline__ T dz_knot(const Ctx<T, ROBOT> &C, int k, T (&mus)[3],
             const T vL[3] = {-(rdx[6] + ex[6]), -(rdx[7] + ex[7]), -(rdx[8] + ex[8])};
             tr_local(C, Lk, z1, dsl, iden, vL, -rdt, rh9, dx + 6, dtt, dlt, dls);
         }
+        // the rows' g'dz use the correction itself (ds = -r_i - g'dz is linear in the solve)
 #pragma unroll
-        for (int i = 0; i < 9; ++i) dxo[i * ld] = dx[i];
-        dto[0] = dtt;
+        for (int i = 0; i < 9; ++i) dxo[i * ld] = ACC ? dxo[i * ld] + dx[i] : dx[i];
+        dto[0] = ACC ? dto[0] + dtt : dtt;
 #pragma unroll
         for (int j = 0; j < 8; ++j)
             emit(j, true, tr_sign<T>(j, 0) * dx[6] + tr_sign<T>(j, 1) * dx[7] + tr_sign<T>(j, 2) * dx[8] + C.cw * dtt,
@@ -1557,7 +1618,7 @@ __device__ __forceinline__ T dz_knot(const Ctx<T, ROBOT> &C, int k, T (&mus)[3],
         const T hf = hu ? T(1) : T(0);
         for (int q = 0; q < NUPC; ++q) du[q] = (-wuv[NUPC * c + q] - au[q]) * hf;
         if (hu)
-            for (int q = 0; q < NUPC; ++q) duo[(NUPC * c + q) * ld] = du[q];
+            for (int q = 0; q < NUPC; ++q) duo[(NUPC * c + q) * ld] = ACC ? duo[(NUPC * c + q) * ld] + du[q] : du[q];
         for (int i = 0; i < 3; ++i) vf[i] = -(rduv[NUPC * c + FO + i] + ec[FO + i]) * hf;
         T z[4];
         for (int r = 0; r < 4; ++r) z[r] = Gw[r][0] * vf[0] + Gw[r][1] * vf[1] + Gw[r][2] * vf[2] + rh4[r];
@@ -1591,6 +1652,124 @@ __device__ PHASE_ATTR T phase_dz(const Ctx<T, ROBOT> &C, int k, int corr, bool i
                              ws + WF(dx) * KPC + k, ws + WF(dt) * KPC + k,
                              ws + WF(du) * KPC + k, ws + (corr ? WF(ds) : WF(dsa)) * KPC + k,
                              ws + (corr ? WF(dl) : WF(dla)) * KPC + k);
+}
+
+// the refinement's correction added to the corrector direction (dz_knot<ACC>): same inputs as the
+// corrector's, whose fields phase_lres has overwritten with the Newton system's residuals
+template <typename T, int ROBOT> __device__ PHASE_ATTR T phase_dz_refine(const Ctx<T, ROBOT> &C, int k) {
+    const int kc = k < C.N ? k : 0;
+    T *ws = C.ws;
+    T mus[3] = {T(0), T(0), T(0)};
+    return dz_knot<T, ROBOT, true>(C, k, mus, false, C.stage + kc, ws + WF(rh) * KPC + k, ws + WF(rdx) * KPC + k,
+                                   ws + WF(rdt) * KPC + k, ws + WF(wu) * KPC + kc, ws + WF(s) * KPC + k,
+                                   ws + WF(l) * KPC + k, ws + WF(rdi) * KPC + k, ws + WF(rdu) * KPC + kc,
+                                   ws + WF(dx) * KPC + k, ws + WF(dt) * KPC + k, ws + WF(du) * KPC + k,
+                                   ws + WF(ds) * KPC + k, ws + WF(dl) * KPC + k);
+}
+
+// (5e) residual of the Newton system at the corrector direction, knot k (iterative refinement):
+//   e_x = W dx + E'_x dnu + G'_x dl + r_dx     e_t = cw 1'dl_TR - dl_sl + r_dt
+//   e_u = W du + E'_u dnu + G'_u dl + r_du     e_e = E dz + r_e
+//   e_i = G dz + ds + r_i                      e_c = s dl + lambda ds + r_c
+// with r_c = s lambda + ds_aff dl_aff - sigma mu.  The residuals overwrite r_dx, r_dt, r_du, r_e,
+// r_i and (e_c) the dsa field, which the corrector no longer needs; dnu (in LDS) is saved to the
+// dn0 field.  The same w / Schur / direction phases then solve for the correction.
+template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_lres(const Ctx<T, ROBOT> &C, int k, T sigma_mu) {
+    using S = Stage<ROBOT>;
+    using R_ = Rows<ROBOT>;
+    constexpr int NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
+    const int N = C.N;
+    const bool hu = k < N;
+    const int kc = hu ? k : 0;
+    const SV<const T> st = C.st(kc);
+    const unsigned msk = C.cmask(k);
+    const LdsT<T> *vb = C.vb;
+    T dk[9], d1[9], dx[9], dx1[9], du[NU], rdx[9], rdu[NU], w[3];
+    for (int i = 0; i < 9; ++i) { dk[i] = vb[k * 9 + i]; d1[i] = vb[(k + 1) * 9 + i]; }
+    ldv(C.kv(WF(dx), k), dx);
+    ldv(C.kv(WF(dx), hu ? k + 1 : k), dx1);
+    ldv(C.kv(WF(du), kc), du);
+    ldv(C.kv(WF(rdx), k), rdx);
+    ldv(C.kv(WF(rdu), kc), rdu);
+    ldv(st + S::W, w);
+    const T dt = C.kv(WF(dt), k)[0], rdt = C.kv(WF(rdt), k)[0];
+    T re0[9], re1[9];
+    ldv(C.bv(WF(rde), k == N ? N + 1 : 0), re0);
+    ldv(C.bv(WF(rde), hu ? 1 + k : 0), re1);
+    // E' dnu at knot k (as in resid_knot)
+    T ex[9], eu[NU], a[9];
+    opAT(w, C.beta, d1, a);
+    opBT<T, ROBOT>(st, d1, eu);
+    for (int i = 0; i < 9; ++i) ex[i] = (k == 0 ? dk[i] : -dk[i]) + (hu ? a[i] : T(0)) + (k == N ? d1[i] : T(0));
+    // rows: e_i, e_c and G' dl
+    T gL[3] = {T(0), T(0), T(0)}, gt = T(0), gu[NU];
+    for (int i = 0; i < NU; ++i) gu[i] = T(0);
+    const SV<T> sS = C.kv(WF(s), k), lS = C.kv(WF(l), k), dsS = C.kv(WF(ds), k), dlS = C.kv(WF(dl), k),
+                riS = C.kv(WF(rdi), k), caS = C.kv(WF(dsa), k);
+    auto row = [&](int r, bool pr, T g) {   // g = g'dz of the row; returns dl (0 on absent rows)
+        const T sr = sS[r], lr = lS[r], dsr = dsS[r], dlr = dlS[r], ri = riS[r], pa = caS[r];
+        const T ei = g + dsr + ri;
+        const T ec = fma(sr, dlr, fma(lr, dsr, fma(sr, lr, pa - sigma_mu)));
+        riS[r] = pr ? ei : T(0);
+        caS[r] = pr ? ec : T(0);
+        return pr ? dlr : T(0);
+    };
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const T dlr = row(j, true, tr_sign<T>(j, 0) * dx[6] + tr_sign<T>(j, 1) * dx[7] + tr_sign<T>(j, 2) * dx[8] + C.cw * dt);
+        for (int i = 0; i < 3; ++i) gL[i] += tr_sign<T>(j, i) * dlr;
+        gt += C.cw * dlr;
+    }
+    gt -= row(8, true, -dt);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const bool pr = hu && ((msk >> c) & 1u);
+        const auto cs = st + (S::CON + S::CS * c);
+        const T *f = du + NUPC * c + FO;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const T g0 = cs[S::G + 3 * r], g1 = cs[S::G + 3 * r + 1], g2 = cs[S::G + 3 * r + 2];
+            const T dlr = row(R_::FR + 4 * c + r, pr, g0 * f[0] + g1 * f[1] + g2 * f[2]);
+            gu[NUPC * c + FO] += g0 * dlr;
+            gu[NUPC * c + FO + 1] += g1 * dlr;
+            gu[NUPC * c + FO + 2] += g2 * dlr;
+        }
+        if (ROBOT == 1) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int dd = q / 2;
+                const T dcop = du[NUPC * c + dd];
+                const T dlr = row(R_::CP + 4 * c + q, pr, (q % 2 == 0) ? dcop : -dcop);
+                gu[NUPC * c + dd] += (q % 2 == 0) ? dlr : -dlr;
+            }
+        }
+    }
+    // dual rows
+    T ox[9];
+    for (int i = 0; i < 9; ++i) ox[i] = C.Wx(i) * dx[i] + ex[i] + (i >= 6 ? gL[i - 6] : T(0)) + rdx[i];
+    stv(C.kv(WF(rdx), k), ox);
+    C.kv(WF(rdt), k)[0] = gt + rdt;
+    if (hu) {
+        T ou[NU];
+        for (int i = 0; i < NU; ++i) ou[i] = C.Wu(i) * du[i] + eu[i] + gu[i] + rdu[i];
+        stv(C.kv(WF(rdu), k), ou);
+    }
+    // equality rows
+    if (hu) {
+        T ax[9], bu[9], oe[9];
+        opA(w, C.beta, dx, ax);
+        opB<T, ROBOT>(st, du, bu);
+        for (int i = 0; i < 9; ++i) oe[i] = ax[i] + bu[i] - dx1[i] + re1[i];
+        stv(C.bv(WF(rde), 1 + k), oe);
+    }
+    if (k == 0 || k == N) {
+        T ob[9];
+        for (int i = 0; i < 9; ++i) ob[i] = dx[i] + re0[i];
+        stv(C.bv(WF(rde), k == 0 ? 0 : N + 1), ob);
+    }
+    // dnu saved for the sum after the correction solve
+    stv(C.bv(WF(dn0), k), dk);
+    if (k == N) stv(C.bv(WF(dn0), N + 1), d1);
 }
 
 // z, nu, s, lambda += a * direction (dnu from the LDS vector)
@@ -1697,6 +1876,33 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_init_shift(con
     }
 }
 
+// One step of iterative refinement of the corrector direction; returns the new step bound.
+// (Inlined: as an outlined call, the registers live across it were reloaded from scratch all over
+// the Newton step.)
+template <typename T, int ROBOT>
+__device__ __forceinline__ T refine_direction(const Ctx<T, ROBOT> &C, T sigma_mu, LdsT<T> *ring, LdsT<T> *shl,
+                                                        T *red) {
+    const int tid = threadIdx.x, K1 = C.N + 1, NB = C.N + 2, NBm = NB / 2;
+    for (int k = tid; k < K1; k += NT) phase_lres<T, ROBOT>(C, k, sigma_mu);
+    __syncthreads();
+    for (int k = tid; k < K1; k += NT) phase_w<T, ROBOT>(C, k, 2, T(0));
+    __syncthreads();
+    tw_solve_elim<T>(C.So, NB, NBm, C.vb, ring);
+    __syncthreads();
+    if (tid < 64) tw_solve_meet<T>(C.Sd, C.So, NB, NBm, C.vb, shl);
+    __syncthreads();
+    tw_solve_local<T>(C.Sd, NB, NBm, C.vb);
+    __syncthreads();
+    tw_solve_back<T>(C.So, NB, NBm, C.vb, ring);
+    __syncthreads();
+    T ar[1] = {T(1)};
+    for (int k = tid; k < K1; k += NT) ar[0] = fmin(ar[0], phase_dz_refine<T, ROBOT>(C, k));
+    block_reduce<T, NT, 1, 2>(ar, red);   // (its barriers order the dnu reads before the sum)
+    for (int e = tid; e < NB * 9; e += NT) C.vb[e] += C.ws[(WF(dn0) + e % 9) * KPC + e / 9];
+    __syncthreads();
+    return ar[0];
+}
+
 // ------------------------------------------------------------------ kernel
 template <typename T, int ROBOT>
 __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int only_active, int max_iter, T eps_abs, T eps_rel,
@@ -1774,8 +1980,8 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
         for (int i = 0; i < 9; ++i) nu[i] = T(0);
     }
     __syncthreads();
-    int status = CMPC_QP_MAX_ITER, it = 0, stall = 0;
-    T mu_prev = T(-1);
+    int status = CMPC_QP_MAX_ITER, it = 0, stall = 0, n_refine = 0;
+    T mu_prev = T(-1), merit = T(0), prim_prev = T(0);
     // it == 0 is the initialization step (CVXOPT-style): one full Newton step from
     // s = lambda = 1 gives an equality-feasible least-squares start; s and lambda are then
     // shifted by (1 + max violation) where negative.
@@ -1791,14 +1997,29 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
         const T prim = mx[0], dual = mx[1], comp = mx[2], sp = mx[3], sdd = mx[4];
         const T mu = sm2[0] / fmax(sm2[1], T(1));
         const T ep = eps_abs + eps_rel * sp, ed = eps_abs + eps_rel * sdd;
-        const T merit = fmax(prim / ep, fmax(dual / ed, comp / ed));
+        merit = fmax(prim / ep, fmax(dual / ed, comp / ed));
         if (!(merit == merit) || !(mu == mu)) { status = CMPC_QP_NONFINITE; break; }
         if (!init) {
-            if (merit <= T(1)) { status = 1; break; }
-            // stall guard: mu not decreasing for 3 iterations while within 1e3x of tolerance
+            if (merit <= T(1)) { status = CMPC_QP_SOLVED; break; }
+            // primal infeasibility (Farkas, OSQP's test on the diverging multipliers), checked once
+            // the primal residual stagnates away from the solution:
+            // |E'nu + G'lambda| <= eps |(nu, lambda)| and b'nu + h'lambda <= -eps |(nu, lambda)|
+            if (it >= 3 && prim > T(0.9) * prim_prev && merit > T(1e3)) {
+                T cm[2] = {T(0), mx[5]}, cs[1] = {T(0)};
+                for (int k = tid; k < K1; k += NT) phase_cert<T, ROBOT>(C, k, cm, cs[0]);
+                block_reduce<T, NT, 2, 1>(cm, red);
+                block_reduce<T, NT, 1, 0>(cs, red);
+                if (cm[0] <= T(QP_EPS_PINF) * cm[1] && cs[0] <= -T(QP_EPS_PINF) * cm[1]) {
+                    status = CMPC_QP_PRIMAL_INFEASIBLE;
+                    break;
+                }
+            }
+            prim_prev = prim;
+            // stall guard: mu not decreasing for 3 iterations while within 1e3x of the tolerance;
+            // reported as 'solved inaccurate', a failure for the SCP loop as in the reference (Q13)
             stall = (mu_prev >= T(0) && mu >= T(0.5) * mu_prev) ? stall + 1 : 0;
             mu_prev = mu;
-            if (stall >= 3 && merit <= T(1e3)) { status = 1; break; }
+            if (stall >= 3 && merit <= T(1e3)) { status = CMPC_QP_SOLVED_INACCURATE; break; }
         }
         if (it == max_iter) break;
         // ---- Phi factors and the predictor's particular solution (knot-local), then the S blocks
@@ -1854,6 +2075,13 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
                 const T mu_aff = (mus[0] + alpha * (mus[1] + alpha * mus[2])) / fmax(sm2[1], T(1));
                 const T sg = mu_aff / fmax(mu, T(1e-300));
                 sigma_mu = sg * sg * sg * mu;
+            } else if ((alpha < T(QP_REFINE_ALPHA) || stall > 0) && merit < T(QP_REFINE_MERIT)) {
+                // the step collapsed, or mu did not halve in the last iteration, late in the solve:
+                // one step of iterative refinement of the corrector direction (residual of the
+                // Newton system with the exact operators, correction solved with the same
+                // factorization; see oracle/ipm_mirror.py)
+                alpha = refine_direction<T, ROBOT>(C, sigma_mu, ring, shl, red);
+                ++n_refine;
             }
         }
         if (init) {
@@ -1888,6 +2116,8 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
     if (tid == 0) {
         d.qp_status[b] = status;
         d.qp_iters[b] = it;
+        d.qp_merit[b] = merit;
+        d.qp_nref[b] = n_refine;
 #ifdef CMPC_STAMPS
         for (int i = 0; i < 9; ++i) d.stamps[(size_t)b * 16 + i] = t_acc[i];   // 9..11: k_linearize, 12..15: tw_factor_ends
 #endif

@@ -44,10 +44,21 @@ extern "C" {
 #define CMPC_PREC_F64 0
 #define CMPC_PREC_F32 1
 
-/* per-problem SCP / QP status codes (OSQP-compatible values) */
+/* per-problem QP status codes (OSQP's values, src/scp_solver.py:65: only 'solved' counts):
+ *   1  solved: merit = max(prim / eps_p, dual / eps_d, compl / eps_d) <= 1
+ *   2  solved inaccurate: mu stalled for 3 iterations within 1e3 of the tolerance (the final
+ *      merit is reported by cmpc_get_qp_info); a failure for the SCP loop, as in the reference
+ *  -2  iteration cap
+ *  -3  primal infeasible: Farkas certificate |E'nu + G'lambda| <= 1e-6 |(nu, lambda)|,
+ *      b'nu + h'lambda <= -1e-6 |(nu, lambda)| on the diverging multipliers
+ *  -4  dual infeasible: never returned; P > 0 on (x, u) and the only other variable t has cost
+ *      +1 with t >= 0, so the subproblem is bounded below
+ * -10  non-finite values */
 #define CMPC_QP_SOLVED 1
+#define CMPC_QP_SOLVED_INACCURATE 2
 #define CMPC_QP_MAX_ITER (-2)
 #define CMPC_QP_PRIMAL_INFEASIBLE (-3)
+#define CMPC_QP_DUAL_INFEASIBLE (-4)
 #define CMPC_QP_NONFINITE (-10)
 
 #define CMPC_SCP_RUNNING 0
@@ -89,8 +100,8 @@ typedef struct {
 /* QP solver settings (defaults by cmpc_default_qp_settings) */
 typedef struct {
     int32_t max_iter;       /* interior-point iterations (default 60) */
-    double eps_abs;         /* absolute tolerance (fp64 default 1e-11, fp32 1e-6) */
-    double eps_rel;         /* relative tolerance (fp64 default 1e-11, fp32 1e-6) */
+    double eps_abs;         /* absolute tolerance (fp64 default 1e-10, fp32 1e-6) */
+    double eps_rel;         /* relative tolerance (fp64 default 1e-10, fp32 1e-6) */
     double step_fraction;   /* fraction-to-boundary (default 0.99) */
 } cmpc_qp_settings;
 
@@ -175,6 +186,9 @@ int cmpc_export_qp(cmpc_handle h, int b, double *P_x, int32_t *P_i, int32_t *P_p
                    int32_t *A_i, int32_t *A_p, double *l, double *u);
 /* z in the reference's variable layout (B, n) and y in its row layout (B, m). */
 int cmpc_get_qp_solution(cmpc_handle h, double *z, double *y, int32_t *status, int32_t *iters);
+/* Per-problem exit data of the last QP solve: final merit (<= 1 when solved) and the number of
+ * iterative-refinement steps taken (B entries each; NULL skips). */
+int cmpc_get_qp_info(cmpc_handle h, double *merit, int32_t *n_refine);
 int cmpc_get_solution(cmpc_handle h, double *X, double *U, double *K, double *Sigma, int32_t *n_accepted,
                       int32_t *iterations, int32_t *scp_status, double *weight, double *radius);
 int cmpc_get_iteration_log(cmpc_handle h, double *tr_norm, double *rho, int32_t *qp_status,
@@ -197,6 +211,29 @@ int cmpc_get_qp_iterations_total(cmpc_handle h, int64_t *total);
 /* Diagnostic builds (libcmpc_diag.so, -DCMPC_STAMPS): per-problem shader-cycle counters of the
  * QP kernel's phases, (B, 16); zeros in the production library. */
 int cmpc_debug_stamps(cmpc_handle h, uint64_t *out);
+
+/* ---- multi-GPU batch split over RCCL (one process per GPU, one handle per process) ----
+ * The problems are independent: nothing crosses GPUs inside the SCP loop.  Rank r owns a
+ * contiguous slice of the global batch; RCCL carries the shared parameters, the max-reduction of
+ * the timed region and the gather of the results.  The reference is single-process
+ * (src/scp_solver.py:118-179); this is the north star's batch split. */
+#define CMPC_COMM_ID_BYTES 128
+/* ncclGetUniqueId: called by rank 0, handed to the other ranks out of band (cmpc/shard.py). */
+int cmpc_comm_get_unique_id(uint8_t *id_out);
+/* ncclCommInitRank on the handle's device (collective over the nranks processes). */
+int cmpc_comm_init(cmpc_handle h, int nranks, int rank, const uint8_t *id);
+int cmpc_comm_destroy(cmpc_handle h);
+/* Broadcast the root's parameter classes (classes holds n_classes entries of capacity; root's
+ * count wins) and install them with cmpc_set_params on every rank. */
+int cmpc_comm_bcast_params(cmpc_handle h, int root, int n_classes, cmpc_params *classes);
+/* In-place elementwise max over ranks of n doubles (also the barrier of the timed region). */
+int cmpc_comm_allreduce_max(cmpc_handle h, double *v, int n);
+/* Gather every rank's accepted solutions and per-problem statuses to root, rank-major (= the
+ * global problem order of contiguous slices).  All ranks must hold the same batch size B; root's
+ * buffers hold nranks * B problems: X (.., N+1, 9), U (.., N, nu), scp_status, iterations,
+ * qp_status (NULL skips).  Non-root ranks may pass NULL. */
+int cmpc_comm_gather_solution(cmpc_handle h, int root, double *X, double *U, int32_t *scp_status,
+                              int32_t *iterations, int32_t *qp_status);
 
 #ifdef __cplusplus
 }

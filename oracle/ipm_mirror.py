@@ -14,6 +14,23 @@ Structured QP per problem (all blocks per knot k):
 Mehrotra predictor-corrector.  The Newton system is reduced to the dual Schur complement
 S = E Phi^-1 E' (Phi = H + G'DG is block diagonal per knot; t is eliminated in each knot),
 which is block tridiagonal with N+2 blocks of 9x9 and is factorized by block Cholesky.
+
+Exits (the kernel's status codes, OSQP's values): 1 solved (merit <= 1); 2 solved inaccurate
+(the stall guard: mu not halving for 3 iterations within 1e3 of the tolerance; the host maps it
+to a failure as the reference does for OSQP's 'solved inaccurate', src/scp_solver.py:65-67);
+-3 primal infeasible (Farkas certificate from the multipliers, below); -2 iteration cap;
+-10 non-finite.  Dual infeasibility cannot occur: P > 0 on (x, u) and the only other variable t
+has cost +1 and t >= 0, so no recession direction lowers the cost.
+
+Iterative refinement: near the solution of a degenerate QP (a force pinned by three or four
+active pyramid rows, D = lambda / s ~ 1e9) the push-through solves and the Schur factorization
+lose digits, and the corrector direction stops satisfying its own linear system (TALOS N=200
+problem 280 at its second SCP iteration: the friction rows' linearized complementarity residual
+reaches 3e-5 against mu = 7e-6, the step length collapses to 3e-4 and mu stalls).  When the
+corrector's step length is below ``refine_alpha``, or mu did not halve in the previous iteration,
+late in the solve (merit < ``refine_merit``),
+the residual of the full Newton system is formed with the exact operators and one correction
+is solved with the same factorization (one refinement step).
 """
 import numpy as np
 
@@ -62,7 +79,8 @@ def _fslot(qp):
     return 0 if qp.robot == 'solo12' else 2
 
 
-def solve(qp, eps=1e-11, max_iter=60, eta=0.99, verbose=False, reg=0.0, piv_floor=1e-13, dcap_rel=1e12):
+def solve(qp, eps=1e-11, max_iter=60, eta=0.99, verbose=False, reg=0.0, piv_floor=1e-13, dcap_rel=1e12,
+          refine_alpha=0.5, refine_merit=1e6, eps_pinf=1e-6):
     N, nc, nu, nupc = qp.N, qp.nc, qp.nu, qp.nupc
     fo = _fslot(qp)
     talos = qp.robot != 'solo12'
@@ -134,6 +152,10 @@ def solve(qp, eps=1e-11, max_iter=60, eta=0.99, verbose=False, reg=0.0, piv_floo
     s = [mk * 1.0 + (1 - mk) for mk in masks]
     lam = [mk * 1.0 for mk in masks]
     stall = 0; mu_prev = None
+    n_refine = 0; merit = np.inf; prim_prev = 0.0
+    hs = [qp.btr, np.zeros(N + 1), qp.fh]
+    if talos:
+        hs.append(np.stack([np.broadcast_to(cop_hi, (N, nc, 2)), np.broadcast_to(-cop_lo, (N, nc, 2))], axis=3))
     for it in range(0, max_iter + 1):
         # iteration 0 is the initialization step (CVXOPT-style): one full Newton step from
         # s = lambda = 1 (an equality-constrained least-squares start), then s and lambda are
@@ -165,11 +187,23 @@ def solve(qp, eps=1e-11, max_iter=60, eta=0.99, verbose=False, reg=0.0, piv_floo
         if not init and merit <= 1.0:
             status = 1
             break
-        # stall guard: mu no longer decreasing for 3 iterations while within 1e3x of tolerance
+        # primal infeasibility (Farkas): E'nu + G'lambda -> 0 relative to |(nu, lambda)| while
+        # b'nu + h'lambda < 0 (OSQP's test, on the multipliers, which diverge along the certificate)
+        # (evaluated, as in the kernel, once the primal residual stagnates away from the solution)
+        if not init and it >= 3 and prim > 0.9 * prim_prev and merit > 1e3:
+            ay = max(np.abs(ex + gx).max(), np.abs(gt).max(), np.abs(eu + gu).max())
+            cy = float((e_rhs * nu_).sum() + sum((h * l * mk).sum() for h, l, mk in zip(hs, lam, masks)))
+            ny = max(np.abs(nu_).max(), max(float(l.max()) for l in lam))
+            if ay <= eps_pinf * ny and cy <= -eps_pinf * ny:
+                status = -3
+                break
+        prim_prev = prim
+        # stall guard: mu no longer decreasing for 3 iterations while within 1e3x of tolerance;
+        # reported as 'solved inaccurate' (2), which the SCP loop treats as a failed QP
         stall = stall + 1 if (not init and mu_prev is not None and mu_ >= 0.5 * mu_prev) else 0
         mu_prev = None if init else mu_
         if stall >= 3 and merit <= 1e3:
-            status = 1
+            status = 2
             break
         # ---- factorization ----
         D = [li / si * mk for li, si, mk in zip(lam, s, masks)]
@@ -278,7 +312,7 @@ def solve(qp, eps=1e-11, max_iter=60, eta=0.99, verbose=False, reg=0.0, piv_floo
             du_, _ = u_local(vu, np.zeros((N, nc, 4)), np.zeros((N, nc, 2, 2)) if talos else None)
             return dx, dt_, du_
 
-        def newton(rc):
+        def newton(rc, rdx=rdx, rdt=rdt, rdu=rdu, rde=rde, rdi=rdi):
             rhat = [(ri - c / np.where(mk > 0, li, 1.0)) * mk for ri, c, li, mk in zip(rdi, rc, lam, masks)]
             rcp = rhat[3] if talos else None
             # particular solution w = Phi^-1 (r_d + G'D rhat): local solves with v = -r_d
@@ -318,6 +352,18 @@ def solve(qp, eps=1e-11, max_iter=60, eta=0.99, verbose=False, reg=0.0, piv_floo
                 return 1.0
             return min(1.0, float(np.min(-v[neg] / dv[neg])))
 
+        def lin_res(d, rc):
+            """Residual of the Newton system at direction d (the exact operators)."""
+            dx, dt_, du, dnu, dl, ds = d
+            gx_, gt_, gu_ = GT(dl)
+            ex_, eu_ = ET(dnu)
+            zx = np.zeros_like(dx); zu = np.zeros_like(du)
+            gz = Gz(dx, du, dt_)
+            return (qp.Wx * dx + ex_ + gx_ + rdx, gt_ + rdt, qp.Wu * du + eu_ + gu_ + rdu,
+                    Ez(dx, du) - Ez(zx, zu) + rde,
+                    [(g + dsi + ri) * mk for g, dsi, ri, mk in zip(gz, ds, rdi, masks)],
+                    [(si * dli + li * dsi + c) * mk for si, dli, li, dsi, c, mk in zip(s, dl, lam, ds, rc, masks)])
+
         rc_aff = [si * li * mk for si, li, mk in zip(s, lam, masks)]
         dx, dt_, du, dnu, dl, ds = newton(rc_aff)
         if init:
@@ -339,11 +385,23 @@ def solve(qp, eps=1e-11, max_iter=60, eta=0.99, verbose=False, reg=0.0, piv_floo
         dx, dt_, du, dnu, dl, ds = newton(rc)
         a = min(min(max_step(si, dsi, mk) for si, dsi, mk in zip(s, ds, masks)),
                 min(max_step(li, dli, mk) for li, dli, mk in zip(lam, dl, masks)))
+        if (a < refine_alpha or (stall > 0 and refine_alpha > 0)) and merit < refine_merit:
+            # one step of iterative refinement of the corrector direction
+            d = (dx, dt_, du, dnu, dl, ds)
+            r1, r2, r3, r4, r5, r6 = lin_res(d, rc)
+            c = newton(r6, rdx=r1, rdt=r2, rdu=r3, rde=r4, rdi=r5)
+            dx, dt_, du, dnu = dx + c[0], dt_ + c[1], du + c[2], dnu + c[3]
+            dl = [p + q for p, q in zip(dl, c[4])]
+            ds = [p + q for p, q in zip(ds, c[5])]
+            a = min(min(max_step(si, dsi, mk) for si, dsi, mk in zip(s, ds, masks)),
+                    min(max_step(li, dli, mk) for li, dli, mk in zip(lam, dl, masks)))
+            n_refine += 1
         a = min(1.0, eta * a)
         x = x + a * dx; t = t + a * dt_; u = u + a * du; nu_ = nu_ + a * dnu
         s = [np.where(mk > 0, si + a * dsi, 1.0) for si, dsi, mk in zip(s, ds, masks)]
         lam = [(li + a * dli) * mk for li, dli, mk in zip(lam, dl, masks)]
-    return dict(x=x, u=u, t=t, nu=nu_, lam=lam, s=s, status=status, iters=it, hist=hist)
+    return dict(x=x, u=u, t=t, nu=nu_, lam=lam, s=s, status=status, iters=it, hist=hist, merit=merit,
+                n_refine=n_refine)
 
 
 def to_z(qp, sol):

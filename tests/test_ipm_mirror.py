@@ -1,0 +1,73 @@
+"""CPU: the numpy mirror of the GPU interior-point QP (oracle/ipm_mirror.py) on the cases that
+shaped its exits.  The mirror runs the kernel's algorithm step for step, so these pin the
+algorithm itself without a GPU; the GPU side is tests/test_gpu_qp_status.py.
+
+* TALOS N=200, problem 280 of the BASELINE C4 shard at its second SCP iteration (the first
+  iteration rejects every problem on the trust-region test, so the weight is omega0 * gamma_fail
+  = 500 and the radius stays at 100).  Without iterative refinement the corrector direction
+  loses its accuracy on the pinned friction rows and mu stalls (round 1's GPU failure, status
+  -2 after 60 iterations there; the mirror's stall guard reports it as 'solved inaccurate'); with
+  one refinement step where the step length collapses, the IPM converges to merit <= 1 and
+  matches an independent sparse IPM on the reference-form QP.
+* A primal infeasible trot QP (final vertical momentum below the free-fall bound: the friction
+  pyramid keeps every f_z >= 0): the Farkas certificate exits with -3, and the OSQP restatement
+  (the reference's QP algorithm) reports 'primal infeasible' on the same QP.
+"""
+import numpy as np
+import pytest
+
+from cmpc.synth import make_batch
+from oracle import ipm_mirror as IM
+from oracle import model as M, transcription as T
+from oracle.osqp_admm import solve_qp as admm_qp
+from oracle.sparse_ipm import solve_qp as sparse_ipm_qp
+
+
+def _struct(cfg, N, b, weight, radius, edit=None):
+    pb = make_batch(cfg, N, 1, seed_offset=b)     # seed 1000 * cfg_seed + b: problem b of a batch
+    if edit is not None:
+        edit(pb)
+    p = pb.oracle_problem(0)
+    prm = p['prm']
+    par = pb.params[0]
+    td = M.compute_trajectory_data(p['Xbar'], p['Ubar'], p['logic'], p['pos'], p['rot'], prm)
+    qp = IM.StructQP.from_arrays(N, par.robot, pb.nc, par.Wx, par.Wu, pb.Xbar[0], pb.Ubar[0], td['f_x'], td['f_u'],
+                                 td['dynamics'].T, pb.logic[0], pb.rot[0], par.mu, weight, radius,
+                                 tracking=par.tracking, foot_range=par.foot_range)
+    P, q = T.build_cost(N, prm, p['Xbar'])
+    A, l, u = T.build_constraints(N, prm, p['logic'], p['pos'], p['rot'], p['Xbar'], p['Ubar'], td, weight, radius)
+    return qp, (P, q, A, l, u)
+
+
+def test_talos_problem_280_needs_refinement():
+    N = 200
+    qp, ref_qp = _struct('talos', N, 280, 500.0, 100.0)
+    plain = IM.solve(qp, refine_alpha=0.0)
+    assert plain['status'] == 2 and plain['merit'] > 1.0          # the stall, reproduced on the CPU
+    sol = IM.solve(qp)
+    assert sol['status'] == 1 and sol['merit'] <= 1.0 and sol['n_refine'] >= 1
+    ref = sparse_ipm_qp(*ref_qp)
+    assert ref.info.status == 'solved'
+    nx = 9 * (N + 1)
+    z = IM.to_z(qp, sol)
+    assert np.abs(z[:nx] - ref.x[:nx]).max() <= 1e-8 * np.abs(ref.x[:nx]).max()
+
+
+@pytest.mark.parametrize('cfg,N,b', [('trot', 100, 3), ('bound', 60, 5)])
+def test_refinement_not_triggered_on_regular_problems(cfg, N, b):
+    qp, _ = _struct(cfg, N, b, 100.0, 100.0 if cfg == 'trot' else 50.0)
+    sol = IM.solve(qp)
+    assert sol['status'] == 1 and sol['merit'] <= 1.0 and sol['n_refine'] == 0
+
+
+def _infeasible(pb):
+    N, par = pb.N, pb.params[0]
+    pb.Xbar[0, N, 5] = pb.Xbar[0, 0, 5] + N * par.dt * par.mass * par.gravity - 1.0
+
+
+def test_primal_infeasible_certificate():
+    N = 30
+    qp, ref_qp = _struct('trot', N, 0, 100.0, 100.0, edit=_infeasible)
+    sol = IM.solve(qp)
+    assert sol['status'] == -3 and sol['iters'] <= 20
+    assert admm_qp(*ref_qp).info.status == 'primal infeasible'

@@ -1,23 +1,16 @@
-"""Multi-process sharding (world_size 2, gloo, CPU): slices tile the batch and the gathered
-result equals the single-process result.  The per-shard solver is a deterministic stand-in
-(the device solve itself is covered by the GPU tests)."""
+"""Multi-process plumbing of the batch split (CPU, no GPU): slices tile the batch, the RCCL id
+rendezvous hands rank 0's bytes to every rank over TCP, ``spawn_local`` starts one process per
+rank with the launcher variables and propagates failures, and the rank-major gather order equals
+the global problem order.  The RCCL collectives themselves run in tests/test_gpu_comm.py."""
+import multiprocessing as mp
 import os
-import socket
+import sys
 
 import numpy as np
 import pytest
-import torch.distributed as dist
-import torch.multiprocessing as mp
 
-from cmpc.shard import gather_results, shard_bounds, solve_shard
+from cmpc.shard import ID_BYTES, exchange_id, free_port, shard_bounds, spawn_local
 from cmpc.synth import make_batch
-
-
-def fake_solve(pb):
-    """Per-problem values that depend only on that problem's inputs."""
-    X = pb.Xbar.copy()
-    X[:, :, 0] += pb.logic.sum(axis=(1, 2))[:, None]
-    return dict(X=X, n_accepted=pb.logic[:, 0, 0].astype(np.int32), status=np.ones(pb.B, np.int32))
 
 
 def test_shard_bounds_tile_the_batch():
@@ -31,30 +24,71 @@ def test_shard_bounds_tile_the_batch():
         shard_bounds(4, 2, 2)
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(('127.0.0.1', 0))
-        return s.getsockname()[1]
+def _rdzv_worker(rank, world, port, q):
+    uid = exchange_id(rank, world, lambda: bytes(range(ID_BYTES)) if rank == 0 else None, '127.0.0.1', port,
+                      timeout=30.0)
+    q.put((rank, uid))
 
 
-def _worker(rank, world, port, B, out_path):
-    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
-    dist.init_process_group('gloo', rank=rank, world_size=world)
-    pb = make_batch('trot', 20, B, seed_offset=5)
-    lo, hi, res = solve_shard(pb, rank, world, solve_fn=fake_solve)
-    full = gather_results(lo, hi, res, B, dist)
-    if rank == 0:
-        np.savez(out_path, **full)
-    dist.barrier()
-    dist.destroy_process_group()
+@pytest.mark.parametrize('world', [2, 3])
+def test_rccl_id_rendezvous(world):
+    port = free_port()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rdzv_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=60) for _ in range(world))
+    for p in procs:
+        p.join(timeout=30)
+    assert sorted(got) == list(range(world))
+    assert all(v == bytes(range(ID_BYTES)) for v in got.values())
 
 
-@pytest.mark.parametrize('B', [5, 6])
-def test_gloo_world2_gather_matches_single_process(tmp_path, B):
-    out = str(tmp_path / 'full.npz')
-    mp.start_processes(_worker, args=(2, _free_port(), B, out), nprocs=2, join=True, start_method='spawn')
-    got = dict(np.load(out))
-    ref = fake_solve(make_batch('trot', 20, B, seed_offset=5))
-    assert set(got) == set(ref)
-    for k in ref:
-        assert np.array_equal(got[k], ref[k]), k
+def test_spawn_local_sets_launcher_env(tmp_path):
+    script = tmp_path / 'child.py'
+    script.write_text('import os, sys\n'
+                      'open(os.path.join(sys.argv[1], "r%s" % os.environ["RANK"]), "w").write(\n'
+                      '    " ".join(os.environ[k] for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR")))\n')
+    rc = spawn_local(2, [str(script), str(tmp_path)], timeout=120)
+    assert rc == 0
+    assert (tmp_path / 'r0').read_text() == '0 0 2 127.0.0.1'
+    assert (tmp_path / 'r1').read_text() == '1 1 2 127.0.0.1'
+
+
+def test_spawn_local_propagates_a_failure(tmp_path):
+    script = tmp_path / 'child.py'
+    script.write_text('import os, sys, time\n'
+                      'if os.environ["RANK"] == "1": sys.exit(3)\n'
+                      'time.sleep(60)\n')
+    rc = spawn_local(2, [str(script)], timeout=120)
+    assert rc == 3
+
+
+def test_rank_major_gather_is_the_global_order():
+    """Contiguous slices generated per rank with seed offset lo reproduce the global batch, so the
+    rank-major concatenation of per-rank results (what cmpc_comm_gather_solution returns) is the
+    global problem order."""
+    B, world = 12, 4
+    full = make_batch('trot', 20, B, seed_offset=0)
+    parts = []
+    for r in range(world):
+        lo, hi = shard_bounds(B, r, world)
+        parts.append(make_batch('trot', 20, hi - lo, seed_offset=lo))
+    for k in ('Xbar', 'Ubar', 'logic', 'pos'):
+        assert np.array_equal(np.concatenate([getattr(p, k) for p in parts]), getattr(full, k)), k
+
+
+def test_bench_gpus_flag_spawns_one_process_per_gpu(tmp_path):
+    """``bench.py --gpus 2`` without a launcher starts two ranks (here they stop at the missing GPU /
+    library, which must surface as a nonzero exit code, never as a one-GPU number)."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env.pop('WORLD_SIZE', None)
+    env['HIP_VISIBLE_DEVICES'] = ''
+    r = subprocess.run([sys.executable, os.path.join(root, 'bench.py'), '--gpus', '2', '--steps', '1', '--warmup', '0',
+                        '--batch', '2', '--N', '10', '--no-cpu-baseline'], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode != 0
+    assert '"n_gpus"' not in r.stdout
