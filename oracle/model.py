@@ -121,14 +121,28 @@ def sigma_next(A, B, C, K, Sigma, cov_w, cov_eta, dtype=np.float64):
     return AB @ S_xu @ AB.T + C @ np.asarray(cov_w, t) @ C.T + np.asarray(cov_eta, t)
 
 
-def compute_trajectory_data(X, U, logic, pos, rot, prm, dtype=np.float64):
+def sigma_next_closed_loop(A, B, C, K, Sigma, cov_w, cov_eta, dtype=np.float64):
+    """The same covariance step in the kernel's association (csrc/linearize.hip scan):
+    Acl Sigma Acl' + (C cov_w C' + cov_eta) with Acl = A + B K.  Algebraically identical to
+    ``sigma_next`` ([A B] [[S, S K'], [K S, K S K']] [A B]' = (A + B K) S (A + B K)'); the two
+    roundings differ, and where A + B K has spectral radius ~1 (TALOS with the reference's warm
+    start, quirk Q11) the scan amplifies that difference over the horizon."""
+    t = dtype
+    A, B, C, K, Sigma = (np.asarray(v, t) for v in (A, B, C, K, Sigma))
+    Acl = A + B @ K
+    Qw = C @ np.asarray(cov_w, t) @ C.T + np.asarray(cov_eta, t)
+    return Acl @ Sigma @ Acl.T + Qw
+
+
+def compute_trajectory_data(X, U, logic, pos, rot, prm, dtype=np.float64, assoc='reference'):
     """Per-knot linearization + LQR + covariance scan (src/centroidal_model.py:257-291).
 
     The reference also propagates Cov_dx / Cov_du tensors of shape (N+1, 9, 9, {9,nu}, N+1);
     they are identically zero (``Sigma_next_fun`` is a constant closure, :239-240), so the
     oracle returns them only when ``with_cov_grads`` is requested by a test.
     Returns dict(dynamics (9,N), LQR_gains (N,nu,9), f_x (N,9,9), f_u (N,9,nu),
-    f_w (N,9,3nc), Covs (N+1,9,9)).
+    f_w (N,9,3nc), Covs (N+1,9,9)).  ``assoc='closed_loop'`` evaluates the covariance step in the
+    kernel's association (``sigma_next_closed_loop``) instead of the reference's.
     """
     t = dtype
     N = U.shape[1]; nu = U.shape[0]; nc = prm['nc']
@@ -141,7 +155,8 @@ def compute_trajectory_data(X, U, logic, pos, rot, prm, dtype=np.float64):
         f = integrate_one_step(x, u, pos[k], logic[k], rot[k], prm, t)
         A, B, C = jacobians(x, u, pos[k], logic[k], rot[k], prm, t)
         K = lqr_gain(A, B, prm['Q'], prm['R'], 2, t)
-        Covs[k + 1] = sigma_next(A, B, C, K, Covs[k], prm['cov_w'], prm['cov_eta'], t)
+        step = sigma_next if assoc == 'reference' else sigma_next_closed_loop
+        Covs[k + 1] = step(A, B, C, K, Covs[k], prm['cov_w'], prm['cov_eta'], t)
         dyn[:, k] = f; fx[k] = A; fu[k] = B; fw[k] = C; K_all[k] = K
     return dict(dynamics=dyn, LQR_gains=K_all, f_x=fx, f_u=fu, f_w=fw, Covs=Covs)
 

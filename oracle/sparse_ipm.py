@@ -14,7 +14,7 @@ from scipy.sparse.linalg import splu
 from .osqp_admm import Info, Result
 
 
-def solve_qp(P, q, A, l, u, eps=1e-11, max_iter=80, eta=0.99, reg=1e-12):
+def solve_qp(P, q, A, l, u, eps=1e-11, max_iter=300, eta=0.99, reg=1e-12):
     P = sparse.csc_matrix(P); A = sparse.csr_matrix(A)
     n, m = P.shape[0], A.shape[0]
     l = np.asarray(l, float); u = np.asarray(u, float)

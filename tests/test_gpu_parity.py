@@ -2,7 +2,8 @@
 
 Tolerances (stated per quantity):
   * linearization fp64: f/A/B/C bit-for-bit up to 1e-15 abs; K, Sigma 1e-11 relative to their max
-    (TALOS Sigma 1e-3: the covariance scan is ill-conditioned there, see the test).
+    (TALOS Sigma 1e-4 against the kernel's association: the covariance scan is ill-conditioned
+    there, see the test).
     fp32: 2e-6 relative (f, A, B) / 1e-3 relative (K, Sigma; fp32 LQR solves).
   * assembly: the exported CSC equals the oracle's (reference row order) to 1e-13 (fp64).
   * QP: the GPU solution's KKT residuals on the reference-form QP (prim <= 1e-8, dual <= 1e-6 x
@@ -53,10 +54,17 @@ def test_linearization_fp64(cfg, N, B):
         np.testing.assert_allclose(lin['C'][b], td['f_w'], rtol=0, atol=1e-15)
         np.testing.assert_allclose(lin['K'][b], td['LQR_gains'], rtol=0, atol=1e-11 * np.abs(td['LQR_gains']).max())
         # TALOS: with the reference's TALOS warm start (quirk Q11) the 2-step LQR leaves A + BK with
-        # spectral radius ~1, and the covariance scan amplifies rounding: a 1e-15 relative change
-        # of K moves Sigma_N by ~1.6e-5 relative (measured with the oracle alone)
-        stol = 1e-11 if cfg != 'talos' else 1e-3
-        np.testing.assert_allclose(lin['Sigma'][b], td['Covs'], rtol=0, atol=stol * np.abs(td['Covs']).max())
+        # spectral radius 1, and the covariance scan amplifies rounding: the reference's association
+        # and the kernel's (A + BK) S (A + BK)' differ by ~8e-6 relative at N=50 in the oracle alone
+        # (tests/test_host.py::test_talos_covariance_scan_sensitivity), so the bound is 1e-4 against
+        # the oracle evaluated in the kernel's association; Solo12 holds 1e-11 either way
+        if cfg == 'talos':
+            p = pb.oracle_problem(b)
+            cl = M.compute_trajectory_data(p['Xbar'], p['Ubar'], p['logic'], p['pos'], p['rot'], p['prm'],
+                                           assoc='closed_loop')['Covs']
+            np.testing.assert_allclose(lin['Sigma'][b], cl, rtol=0, atol=1e-4 * np.abs(cl).max())
+        else:
+            np.testing.assert_allclose(lin['Sigma'][b], td['Covs'], rtol=0, atol=1e-11 * np.abs(td['Covs']).max())
     s.close()
 
 
@@ -142,8 +150,9 @@ def test_qp_fp32_tolerance():
     s.close()
 
 
-@pytest.mark.parametrize('cfg,N,B', [('trot', 30, 3), ('bound', 30, 2), ('talos', 40, 2)])
+@pytest.mark.parametrize('cfg,N,B', [('trot', 50, 1), ('trot', 30, 3), ('bound', 30, 2), ('talos', 40, 2)])
 def test_solve_scp_matches_oracle(cfg, N, B):
+    """(trot, 50, 1) is BASELINE C1, the reference's own CPU case, on the GPU."""
     pb, s = _solver(cfg, N, B)
     n = s.solve_scp(fixed_iters=False)
     sol = s.solution()
