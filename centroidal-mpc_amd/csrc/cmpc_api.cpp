@@ -6,6 +6,7 @@
 #include <array>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <tuple>
@@ -17,6 +18,8 @@
 
 namespace cmpc {
 template <typename T, int R> __global__ void k_linearize(DevBuf<T>, int);
+template <typename T, int R> __global__ void k_lin_knots(DevBuf<T>, int);
+template <typename T, int R> __global__ void k_cov_scan(DevBuf<T>, int);
 template <typename T, int R> __global__ void k_assemble(DevBuf<T>, int);
 template <typename T, int R> __global__ void k_qp_ipm(DevBuf<T>, int, int, T, T, T);
 template <typename T> __global__ void k_interpolate(DevBuf<T>, int, int, T *, T *);
@@ -96,7 +99,14 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
     if (B == 0) return;
     switch (phase) {
     case 0:
-        hipLaunchKernelGGL((k_linearize<T, R>), dim3(B), dim3(256), 0, h->stream, d, only_active);
+        if (h->lin_lane) {   // one knot per lane (diagonal R), then the per-problem covariance scan
+            const long n = (long)B * h->N;
+            hipLaunchKernelGGL((k_lin_knots<T, R>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream, d,
+                               only_active);
+            hipLaunchKernelGGL((k_cov_scan<T, R>), dim3(B), dim3(64), 0, h->stream, d, only_active);
+        } else {
+            hipLaunchKernelGGL((k_linearize<T, R>), dim3(B), dim3(256), 0, h->stream, d, only_active);
+        }
         break;
     case 1: {
         const long n = (long)B * (h->N + 1);
@@ -329,6 +339,15 @@ int cmpc_set_params(cmpc_handle h, int n_classes, const cmpc_params *classes) {
         }
         h->hparams.assign(classes, classes + n_classes);
         h->n_classes = n_classes;
+        // the knot-per-lane linearization needs a diagonal LQR weight R (every reference config);
+        // CMPC_LIN_LEGACY=1 forces the workgroup-per-problem kernel
+        bool diag = true;
+        for (int i = 0; i < n_classes; ++i)
+            for (int r = 0; r < 12; ++r)
+                for (int c = 0; c < 12; ++c)
+                    if (r != c && classes[i].R[r * 12 + c] != 0.0) diag = false;
+        const char *leg = std::getenv("CMPC_LIN_LEGACY");
+        h->lin_lane = diag && !(leg && leg[0] == '1');
         const int nw = 3 * h->NC;
         if (h->params) { HIPCHK(hipFree(h->params)); h->allocs.erase(std::find(h->allocs.begin(), h->allocs.end(), h->params)); }
         if (h->prec == CMPC_PREC_F64) {

@@ -50,6 +50,7 @@ struct cmpc_handle_s {
          *Xacc = nullptr, *Uacc = nullptr, *Kacc = nullptr, *Sacc = nullptr, *stamps = nullptr, *Xlin = nullptr,
          *Ulin = nullptr;
     int scp_mode = CMPC_SCP_MODE_REFERENCE;
+    bool lin_lane = true;   // knot-per-lane linearization (diagonal R); else k_linearize
     // RCCL communicator of the batch split (comm.cpp); nullptr until cmpc_comm_init
     void *comm = nullptr;
     int comm_rank = 0, comm_size = 1;

@@ -1,0 +1,463 @@
+// Linearization with one knot per lane (the default path; diagonal LQR weight R, as in every
+// reference config): f, A, B, C (closed form), the LQR gain K of two Riccati steps from P = Q, and
+// the covariance-scan helpers Acl = A + B K, Qw = C W C' + eta, all in one lane's registers.
+//
+// Replaces Centroidal_model.compute_everything / integrate_model_one_step (reference
+// src/centroidal_model.py:189-241, compute_lqr_feedback_gains :217-228): every knot of every
+// problem is independent, so the wave holds 64 knots and every lane runs the same straight-line
+// program on its own knot (no LDS, no barriers).  The Riccati step is taken in information form,
+// which only inverts 9x9 SPD matrices instead of the reference's 12x12 R + B'PB:
+//   P+ = Q + A' P A - A'PB (R + B'PB)^-1 B'PA = Q + A' N^-1 A,   N = P^-1 + B R^-1 B'
+//   K  = -(R + B'P2 B)^-1 B'P2 A = -R^-1 B' N2^-1 A
+// (Woodbury / push-through identities; B has rows 3..8 only, so B R^-1 B' is a 6x6 block G).
+// A = [[I, beta I, 0], [0, I, 0], [W, 0, I]] (beta = dt/m, W = dt [sum a_i f_i]x) is used through
+// its block structure, never as a dense matrix.  The covariance scan itself (sequential over the
+// knots) runs in k_cov_scan, one wave per problem on the matrix cores.
+//
+// Non-diagonal R falls back to k_linearize (linearize.hip), which works with R + B'PB directly.
+#include "common.hpp"
+
+namespace cmpc {
+
+__device__ __forceinline__ constexpr int sp9(int i, int j) { return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i; }
+
+template <typename T> __device__ __forceinline__ T rcp_l(T p) {
+    T r;
+    if constexpr (sizeof(T) == 8) r = __builtin_amdgcn_rcp(p); else r = __builtin_amdgcn_rcpf(p);
+    r = fma(r, fma(-p, r, T(1)), r);
+    return fma(r, fma(-p, r, T(1)), r);
+}
+
+// Inverse of a 9x9 SPD matrix (packed lower, sp9) by Cholesky: M^-1 = L^-T L^-1.  In registers,
+// fully unrolled (compile-time indices).
+template <typename T> __device__ __forceinline__ void inv_spd9(const T (&m)[45], T (&out)[45]) {
+    T L[45], id[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+        T d = m[sp9(j, j)];
+#pragma unroll
+        for (int q = 0; q < j; ++q) d = fma(-L[sp9(j, q)], L[sp9(j, q)], d);
+        const T ljj = sqrt(d);
+        id[j] = rcp_l(ljj);
+        L[sp9(j, j)] = ljj;
+#pragma unroll
+        for (int i = j + 1; i < 9; ++i) {
+            T v = m[sp9(i, j)];
+#pragma unroll
+            for (int q = 0; q < j; ++q) v = fma(-L[sp9(i, q)], L[sp9(j, q)], v);
+            L[sp9(i, j)] = v * id[j];
+        }
+    }
+    T Li[45];   // L^-1, lower
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+        Li[sp9(j, j)] = id[j];
+#pragma unroll
+        for (int i = j + 1; i < 9; ++i) {
+            T v = T(0);
+#pragma unroll
+            for (int k = j; k < i; ++k) v = fma(L[sp9(i, k)], Li[sp9(k, j)], v);
+            Li[sp9(i, j)] = -v * id[i];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 9; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j) {
+            T v = T(0);
+#pragma unroll
+            for (int k = i; k < 9; ++k) v = fma(Li[sp9(k, i)], Li[sp9(k, j)], v);
+            out[sp9(i, j)] = v;
+        }
+}
+
+// Column j of M A (row k), for the centroidal A: column block c: M[:,c] + M[:,L] W; block l:
+// beta M[:,c] + M[:,l]; block L: M[:,L].  Wm = W (3x3, dt [w]x).
+template <typename T>
+__device__ __forceinline__ T MA_at(const T (&M)[45], T beta, const T (&Wm)[3][3], int k, int j) {
+    if (j < 3) return M[sp9(k, j)] + M[sp9(k, 6)] * Wm[0][j] + M[sp9(k, 7)] * Wm[1][j] + M[sp9(k, 8)] * Wm[2][j];
+    if (j < 6) return fma(beta, M[sp9(k, j - 3)], M[sp9(k, j)]);
+    return M[sp9(k, j)];
+}
+
+// out = Q + A' M A (packed lower; Q diagonal-or-dense from the parameters)
+template <typename T>
+__device__ __forceinline__ void atma(const T (&M)[45], T beta, const T (&Wm)[3][3], const T *Q, T (&out)[45]) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j) {
+            const int rb = i / 3, ii = i % 3;
+            T v;
+            if (rb == 0)
+                v = MA_at(M, beta, Wm, ii, j) + Wm[0][ii] * MA_at(M, beta, Wm, 6, j) + Wm[1][ii] * MA_at(M, beta, Wm, 7, j) +
+                    Wm[2][ii] * MA_at(M, beta, Wm, 8, j);
+            else if (rb == 1)
+                v = fma(beta, MA_at(M, beta, Wm, ii, j), MA_at(M, beta, Wm, 3 + ii, j));
+            else
+                v = MA_at(M, beta, Wm, 6 + ii, j);
+            out[sp9(i, j)] = v + Q[i * 9 + j];
+        }
+}
+
+// rows 3..8 of the per-contact input matrix B_c (6 x NUPC) of contact c
+template <typename T, int ROBOT> struct ContactB {
+    static constexpr int NUPC = Robot<ROBOT>::NUPC;
+    T b[6][NUPC];
+};
+
+template <typename T, int ROBOT>
+__device__ __forceinline__ void contact_B(T dta, const T (&lev)[3], const T *f, const T *Rc, ContactB<T, ROBOT> &B) {
+    constexpr int NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
+    const T sk[3][3] = {{T(0), -lev[2], lev[1]}, {lev[2], T(0), -lev[0]}, {-lev[1], lev[0], T(0)}};
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+        for (int q = 0; q < NUPC; ++q) B.b[a][q] = T(0);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        B.b[q][FO + q] = dta;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) B.b[3 + r][FO + q] = dta * sk[r][q];
+    }
+    if (ROBOT == 1) {
+        const T fs[3][3] = {{T(0), -f[2], f[1]}, {f[2], T(0), -f[0]}, {-f[1], f[0], T(0)}};
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+#pragma unroll
+            for (int q = 0; q < 2; ++q)   // d/dcop [(R2 cop) x f] = -[f]x R[:, q]
+                B.b[3 + r][q] = -dta * (fs[r][0] * Rc[0 * 3 + q] + fs[r][1] * Rc[1 * 3 + q] + fs[r][2] * Rc[2 * 3 + q]);
+            B.b[3 + r][5] = dta * Rc[r * 3 + 2];   // tau
+        }
+    }
+}
+
+template <typename T, int ROBOT>
+__global__ void __launch_bounds__(256, 1) k_lin_knots(DevBuf<T> d, int only_active) {
+    constexpr int NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO, NW = 3 * NC;
+    const int N = d.N;
+    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (long)d.B * N) return;
+    const int b = (int)(t / N), k = (int)(t % N);
+    if (only_active && !d.scp[b].active) return;
+    const DevParams<T> &prm = d.params[d.class_id[b]];
+    const size_t kn = (size_t)b * N + k;
+    // ---- inputs of the knot (the linearization point and the contact data)
+    T x[9], u[NU], p[3 * NC], rot[9 * NC], a[NC];
+    const T *xs = d.Xlin + ((size_t)b * (N + 1) + k) * 9, *us = d.Ulin + kn * NU;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) x[i] = xs[i];
+#pragma unroll
+    for (int i = 0; i < NU; ++i) u[i] = us[i];
+#pragma unroll
+    for (int i = 0; i < 3 * NC; ++i) p[i] = d.pos[kn * 3 * NC + i];
+    if (ROBOT == 1) {
+#pragma unroll
+        for (int i = 0; i < 9 * NC; ++i) rot[i] = d.rot[kn * 9 * NC + i];
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) a[c] = T(d.logic[kn * NC + c]);
+    const T dt = prm.dt, m = prm.mass, beta = dt / m;
+    // levers: p_c - com (+ R_c[:, 0:2] cop_c for TALOS)
+    T lev[NC][3], w[3] = {T(0), T(0), T(0)};
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+#pragma unroll
+        for (int z = 0; z < 3; ++z) {
+            lev[c][z] = p[3 * c + z] - x[z];
+            if (ROBOT == 1) lev[c][z] += rot[9 * c + z * 3] * u[NUPC * c] + rot[9 * c + z * 3 + 1] * u[NUPC * c + 1];
+            w[z] = fma(a[c], u[NUPC * c + FO + z], w[z]);
+        }
+    }
+    // ---- f = x + dt F(x, u)   (src/centroidal_model.py:189-212)
+    {
+        T F[9];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) F[i] = (T(1) / m) * x[3 + i];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) F[3 + i] = w[i];
+        F[5] += m * prm.gravity;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) F[6 + r] = T(0);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const T *f = u + NUPC * c + FO;
+            T lf[3];
+            cross3(lev[c], f, lf);
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                T v = lf[r];
+                if (ROBOT == 1) v += rot[9 * c + r * 3 + 2] * u[NUPC * c + 5];
+                F[6 + r] = fma(a[c], v, F[6 + r]);
+            }
+        }
+        T *fo = d.f + kn * 9;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) fo[i] = x[i] + F[i] * dt;
+    }
+    const T Wm[3][3] = {{T(0), -dt * w[2], dt * w[1]}, {dt * w[2], T(0), -dt * w[0]}, {-dt * w[1], dt * w[0], T(0)}};
+    // ---- A, B, C (jacfwd at :230-232), closed form
+    {
+        T *Ao = d.A + kn * 81;
+#pragma unroll
+        for (int i = 0; i < 9; ++i)
+#pragma unroll
+            for (int j = 0; j < 9; ++j) {
+                T v = (i == j) ? T(1) : T(0);
+                if (i < 3 && j == i + 3) v = beta;
+                if (i >= 6 && j < 3) v = Wm[i - 6][j];
+                Ao[i * 9 + j] = v;
+            }
+        T *Bo = d.Bu + kn * 9 * NU, *Co = d.C + kn * 9 * NW;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            ContactB<T, ROBOT> Bc;
+            contact_B<T, ROBOT>(dt * a[c], lev[c], u + NUPC * c + FO, rot + 9 * c, Bc);
+#pragma unroll
+            for (int i = 0; i < 9; ++i)
+#pragma unroll
+                for (int q = 0; q < NUPC; ++q) Bo[i * NU + NUPC * c + q] = i < 3 ? T(0) : Bc.b[i - 3][q];
+            const T *f = u + NUPC * c + FO;
+            const T fs[3][3] = {{T(0), -f[2], f[1]}, {f[2], T(0), -f[0]}, {-f[1], f[0], T(0)}};
+#pragma unroll
+            for (int i = 0; i < 9; ++i)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) Co[i * NW + 3 * c + q] = i < 6 ? T(0) : -dt * a[c] * fs[i - 6][q];
+        }
+    }
+    // ---- G = B R^-1 B' (rows 3..8), R diagonal
+    T G[21];   // packed lower 6x6
+#pragma unroll
+    for (int e = 0; e < 21; ++e) G[e] = T(0);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        ContactB<T, ROBOT> Bc;
+        contact_B<T, ROBOT>(dt * a[c], lev[c], u + NUPC * c + FO, rot + 9 * c, Bc);
+#pragma unroll
+        for (int q = 0; q < NUPC; ++q) {
+            const T ri = T(1) / prm.R[(NUPC * c + q) * (NU + 1)];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const T bi = Bc.b[i][q] * ri;
+#pragma unroll
+                for (int j = 0; j <= i; ++j) G[i * (i + 1) / 2 + j] = fma(bi, Bc.b[j][q], G[i * (i + 1) / 2 + j]);
+            }
+        }
+    }
+    // ---- two Riccati steps from P = Q in information form, then N2^-1
+    T P[45], Ni[45];
+#pragma unroll
+    for (int i = 0; i < 9; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j) P[sp9(i, j)] = prm.Q[i * 9 + j];
+#pragma unroll 1
+    for (int it = 0; it < 3; ++it) {
+        T Nm[45];
+        inv_spd9(P, Nm);   // P^-1
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+#pragma unroll
+            for (int j = 0; j <= i; ++j) Nm[sp9(3 + i, 3 + j)] += G[i * (i + 1) / 2 + j];
+        inv_spd9(Nm, Ni);  // N^-1
+        if (it < 2) atma(Ni, beta, Wm, prm.Q, P);
+    }
+    // ---- Y6 = rows 3..8 of N2^-1 A;  K = -R^-1 B' Y6;  Acl = A - E6 G Y6
+    T Y6[6][9];
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int j = 0; j < 9; ++j) Y6[r][j] = MA_at(Ni, beta, Wm, 3 + r, j);
+    {
+        T *Ko = d.K + kn * NU * 9;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            ContactB<T, ROBOT> Bc;
+            contact_B<T, ROBOT>(dt * a[c], lev[c], u + NUPC * c + FO, rot + 9 * c, Bc);
+#pragma unroll
+            for (int q = 0; q < NUPC; ++q) {
+                const T ri = T(1) / prm.R[(NUPC * c + q) * (NU + 1)];
+#pragma unroll
+                for (int j = 0; j < 9; ++j) {
+                    T v = T(0);
+#pragma unroll
+                    for (int r = 0; r < 6; ++r) v = fma(Bc.b[r][q], Y6[r][j], v);
+                    Ko[(NUPC * c + q) * 9 + j] = -ri * v;
+                }
+            }
+        }
+    }
+    {
+        T *Ao = d.Acl + kn * 81;
+#pragma unroll
+        for (int i = 0; i < 9; ++i)
+#pragma unroll
+            for (int j = 0; j < 9; ++j) {
+                T v = (i == j) ? T(1) : T(0);
+                if (i < 3 && j == i + 3) v = beta;
+                if (i >= 6 && j < 3) v = Wm[i - 6][j];
+                if (i >= 3) {
+#pragma unroll
+                    for (int r = 0; r < 6; ++r) {
+                        const int ia = i - 3;
+                        const T g = G[ia >= r ? ia * (ia + 1) / 2 + r : r * (r + 1) / 2 + ia];
+                        v = fma(-g, Y6[r][j], v);
+                    }
+                }
+                Ao[i * 9 + j] = v;
+            }
+    }
+    // ---- Qw = C W C' + eta (C: rows 6..8, -dt a_c [f_c]x)
+    {
+        T Cl[3][NW];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const T *f = u + NUPC * c + FO;
+            const T fs[3][3] = {{T(0), -f[2], f[1]}, {f[2], T(0), -f[0]}, {-f[1], f[0], T(0)}};
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) Cl[r][3 * c + q] = -dt * a[c] * fs[r][q];
+        }
+        T CW[3][NW];
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int j = 0; j < NW; ++j) {
+                T v = T(0);
+#pragma unroll
+                for (int q = 0; q < NW; ++q) v = fma(Cl[r][q], prm.cov_w[q * NW + j], v);
+                CW[r][j] = v;
+            }
+        T *Qo = d.Qw + kn * 81;
+#pragma unroll
+        for (int i = 0; i < 9; ++i)
+#pragma unroll
+            for (int j = 0; j < 9; ++j) {
+                T v = prm.cov_eta[i * 9 + j];
+                if (i >= 6 && j >= 6) {
+#pragma unroll
+                    for (int q = 0; q < NW; ++q) v = fma(CW[i - 6][q], Cl[j - 6][q], v);
+                }
+                Qo[i * 9 + j] = v;
+            }
+    }
+}
+
+// Covariance scan (src/centroidal_model.py:234-238, 266, 284), one wave per problem:
+// Sigma_{k+1} = Acl_k Sigma_k Acl_k' + Qw_k from the per-knot helpers of k_lin_knots.  The
+// per-step blocks stream through LDS in double-buffered chunks of KS steps (each chunk's loads
+// issued a chunk ahead inside one loop iteration); fp64 keeps Sigma in the matrix-core
+// accumulator layout for the whole scan (see linearize.hip).
+constexpr int SKS = 4;
+template <typename T, int ROBOT> __global__ void __launch_bounds__(64, 4) k_cov_scan(DevBuf<T> d, int only_active) {
+    const int b = blockIdx.x;
+    if (b >= d.B) return;
+    if (only_active && !d.scp[b].active) return;
+    constexpr int CH = 2 * SKS * 81;
+    constexpr int PL = (CH + WAVE - 1) / WAVE;
+    __shared__ T buf[2 * CH];
+    __shared__ T S[81], Tm[81];
+    const int lane = threadIdx.x, N = d.N;
+    const T *Acl = d.Acl + (size_t)b * N * 81, *Qw = d.Qw + (size_t)b * N * 81;
+    T reg[PL];
+    auto issue = [&](int c) {
+#pragma unroll
+        for (int r = 0; r < PL; ++r) {
+            const int e = min(lane + r * WAVE, CH - 1), blk = e / 81, w = e % 81;
+            const int k = min(c * SKS + blk % SKS, N - 1);
+            reg[r] = (blk < SKS ? Acl : Qw)[(size_t)k * 81 + w];
+        }
+    };
+    auto land = [&](int c) {
+        T *dst = buf + (c & 1) * CH;
+#pragma unroll
+        for (int r = 0; r < PL; ++r)
+            if (lane + r * WAVE < CH) dst[lane + r * WAVE] = reg[r];
+    };
+    for (int e = lane; e < 81; e += WAVE) {
+        S[e] = T(0);
+        d.Sig[((size_t)b * (N + 1)) * 81 + e] = T(0);
+    }
+    issue(0);
+    land(0);
+    wave_sync();
+    typedef double v4d __attribute__((ext_vector_type(4)));
+    [[maybe_unused]] v4d Sreg = {0.0, 0.0, 0.0, 0.0};
+    const int r16 = lane & 15, q4 = lane >> 4;
+    for (int c = 0; c * SKS < N; ++c) {
+        issue(c + 1);
+        const T *cb = buf + (c & 1) * CH;
+        for (int q = 0; q < SKS; ++q) {
+            const int k = c * SKS + q;
+            if (k >= N) break;
+            const T *Ac = cb + q * 81, *Q = cb + (SKS + q) * 81;
+            if constexpr (sizeof(T) == 8) {
+                double av[3];   // Acl[l & 15][4 kb + (l >> 4)] (zero outside 9 x 9)
+#pragma unroll
+                for (int kb = 0; kb < 3; ++kb) {
+                    const int mm = 4 * kb + q4;
+                    av[kb] = (r16 < 9 && mm < 9) ? Ac[(r16 < 9 ? r16 : 0) * 9 + (mm < 9 ? mm : 0)] : 0.0;
+                }
+                v4d qw;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = q4 + 4 * r;
+                    qw[r] = (i < 9 && r16 < 9) ? Q[(i < 9 ? i : 0) * 9 + (r16 < 9 ? r16 : 0)] : 0.0;
+                }
+                v4d Y = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int kb = 0; kb < 3; ++kb) Y = __builtin_amdgcn_mfma_f64_16x16x4f64(Sreg[kb], av[kb], Y, 0, 0, 0);
+                Sreg = qw;
+#pragma unroll
+                for (int kb = 0; kb < 3; ++kb) Sreg = __builtin_amdgcn_mfma_f64_16x16x4f64(av[kb], Y[kb], Sreg, 0, 0, 0);
+                T *so = d.Sig + ((size_t)b * (N + 1) + k + 1) * 81;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = q4 + 4 * r;
+                    if (i < 9 && r16 < 9) so[i * 9 + r16] = Sreg[r];
+                }
+                continue;
+            }
+            for (int e = lane; e < 81; e += WAVE) {     // Tm = Acl S
+                const int i = e / 9, j = e % 9;
+                T acc = T(0);
+#pragma unroll
+                for (int mm = 0; mm < 9; ++mm) acc = fma(Ac[i * 9 + mm], S[mm * 9 + j], acc);
+                Tm[e] = acc;
+            }
+            wave_sync();
+            T out[2];
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {   // Tm Acl' + Qw
+                const int e = min(lane + r * WAVE, 80), i = e / 9, j = e % 9;
+                T acc = Q[e];
+#pragma unroll
+                for (int mm = 0; mm < 9; ++mm) acc = fma(Tm[i * 9 + mm], Ac[j * 9 + mm], acc);
+                out[r] = acc;
+            }
+            wave_sync();
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const int e = lane + r * WAVE;
+                if (e < 81) {
+                    S[e] = out[r];
+                    d.Sig[((size_t)b * (N + 1) + k + 1) * 81 + e] = out[r];
+                }
+            }
+            wave_sync();
+        }
+        land(c + 1);
+        wave_sync();
+    }
+}
+
+#define INST(T, R)                                                     \
+    template __global__ void k_lin_knots<T, R>(DevBuf<T>, int);      \
+    template __global__ void k_cov_scan<T, R>(DevBuf<T>, int);
+INST(double, 0)
+INST(double, 1)
+INST(float, 0)
+INST(float, 1)
+#undef INST
+
+}  // namespace cmpc
