@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libcmpc_diag.so' if os.environ.get('CMPC_LIB_VARIANT') == 'diag' else 'libcmpc.so')
+_VARIANT = os.environ.get('CMPC_LIB_VARIANT')   # 'diag': the cycle-stamp build (libcmpc_diag.so)
+LIB_PATH = os.path.join(_HERE, 'libcmpc_%s.so' % _VARIANT if _VARIANT else 'libcmpc.so')
 
 ROBOTS = {'solo12': 0, 'TALOS': 1}
 PREC = {'fp64': 0, 'float64': 0, 'f64': 0, 'fp32': 1, 'float32': 1, 'f32': 1}
