@@ -12,14 +12,19 @@
 // (skew vector w_k = dt sum a_i f_i) and B_k (alpha_i = dt a_i, lever_i, TALOS cop/tau
 // columns), friction rows G = (F_mu R')[0:4] (src/constraints.py:171-185) and their upper
 // bounds h (0, or minus the chance-constraint back-off 2 xi G_u sqrt(K Sigma K')_uu,
-// src/constraints.py:186-214).  Thread per knot; HBM-bound: reads ~1.9 KB, writes ~1.3 KB
-// per knot at fp64.  Records are stored field-major per problem (field f of knot k at
-// stage[(b * SIZE + f) * KPC + k]) so the QP kernel's per-knot loads coalesce.
+// src/constraints.py:186-214).  Thread per knot; HBM-bound.  Records are stored field-major per
+// problem (field f of knot k at stage[(b * SIZE + f) * KPC + k]) so the QP kernel's per-knot
+// loads coalesce.
+//
+// FULL = false (the default path): k_lin_knots has already written the fields that depend only on
+// the linearization (r, w, the per-contact alpha / lever / G / cop / tau), so this kernel writes
+// the ones that depend on the warm start and the SCP state: qx, the trust-region bounds, cw and h.
+// FULL = true follows the legacy k_linearize (non-diagonal R) and writes the whole record.
 #include "common.hpp"
 
 namespace cmpc {
 
-template <typename T, int ROBOT>
+template <typename T, int ROBOT, bool FULL>
 __global__ void __launch_bounds__(128) k_assemble(DevBuf<T> d, int only_active) {
     constexpr int NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
     using St = Stage<ROBOT>;
@@ -42,20 +47,24 @@ __global__ void __launch_bounds__(128) k_assemble(DevBuf<T> d, int only_active) 
     }
     if (k == N) return;
     const size_t kn = (size_t)b * N + k;
-    const T *A = d.A + kn * 81, *Bm = d.Bu + kn * 9 * NU, *f = d.f + kn * 9, *ub = d.Ulin + kn * NU;
-    for (int i = 0; i < 9; ++i) {
-        T acc = -f[i];
-        for (int j = 0; j < 9; ++j) acc = fma(A[i * 9 + j], xb[j], acc);
-        for (int j = 0; j < NU; ++j) acc = fma(Bm[i * NU + j], ub[j], acc);
-        st[St::R + i] = acc;
-    }
+    auto em = [&](const T *base, int e) -> T { return base[(size_t)e * d.LS + kn]; };   // element-major
+    const T *ub = d.Ulin + kn * NU;
+    if (FULL)
+        for (int i = 0; i < 9; ++i) {
+            T acc = -em(d.f, i);
+            for (int j = 0; j < 9; ++j) acc = fma(em(d.A, i * 9 + j), xb[j], acc);
+            for (int j = 0; j < NU; ++j) acc = fma(em(d.Bu, i * NU + j), ub[j], acc);
+            st[St::R + i] = acc;
+        }
     const T dt = prm.dt;
     const T *pos = d.pos + kn * 3 * NC, *rot = d.rot + kn * 9 * NC;
     const uint8_t *lg = d.logic + kn * NC;
-    T w[3] = {0, 0, 0};
-    for (int c = 0; c < NC; ++c)
-        for (int q = 0; q < 3; ++q) w[q] += T(lg[c]) * ub[NUPC * c + FO + q];
-    for (int q = 0; q < 3; ++q) st[St::W + q] = dt * w[q];
+    if (FULL) {
+        T w[3] = {0, 0, 0};
+        for (int c = 0; c < NC; ++c)
+            for (int q = 0; q < 3; ++q) w[q] += T(lg[c]) * ub[NUPC * c + FO + q];
+        for (int q = 0; q < 3; ++q) st[St::W + q] = dt * w[q];
+    }
     const T ml = prm.mu / sqrt(T(2));
     const T Fmu[4][3] = {{1, 0, -ml}, {-1, 0, -ml}, {0, 1, -ml}, {0, -1, -ml}};
     for (int c = 0; c < NC; ++c) {
@@ -63,33 +72,35 @@ __global__ void __launch_bounds__(128) k_assemble(DevBuf<T> d, int only_active) 
         const T a = T(lg[c]);
         const T *Rc = rot + 9 * c;
         const T *uc = ub + NUPC * c;
-        cs[St::ALPHA] = dt * a;
-        T lev[3];
-        for (int z = 0; z < 3; ++z) lev[z] = pos[3 * c + z] - xb[z];
-        if (ROBOT == 1)
-            for (int z = 0; z < 3; ++z) lev[z] += Rc[z * 3 + 0] * uc[0] + Rc[z * 3 + 1] * uc[1];
-        for (int z = 0; z < 3; ++z) cs[St::LEVER + z] = lev[z];
-        // friction rows 0..3: (F_mu R')[r, :]
-        for (int r = 0; r < 4; ++r)
-            for (int q = 0; q < 3; ++q) {
-                T g = T(0);
-                for (int z = 0; z < 3; ++z) g = fma(Fmu[r][z], Rc[q * 3 + z], g);
-                cs[St::G + r * 3 + q] = g;
-            }
+        if (FULL) {
+            cs[St::ALPHA] = dt * a;
+            T lev[3];
+            for (int z = 0; z < 3; ++z) lev[z] = pos[3 * c + z] - xb[z];
+            if (ROBOT == 1)
+                for (int z = 0; z < 3; ++z) lev[z] += Rc[z * 3 + 0] * uc[0] + Rc[z * 3 + 1] * uc[1];
+            for (int z = 0; z < 3; ++z) cs[St::LEVER + z] = lev[z];
+            // friction rows 0..3: (F_mu R')[r, :]
+            for (int r = 0; r < 4; ++r)
+                for (int q = 0; q < 3; ++q) {
+                    T g = T(0);
+                    for (int z = 0; z < 3; ++z) g = fma(Fmu[r][z], Rc[q * 3 + z], g);
+                    cs[St::G + r * 3 + q] = g;
+                }
+        }
         T h[4] = {0, 0, 0, 0};
         if (prm.stochastic && k > 0 && lg[c]) {
             // K rows 3c..3c+2 (reference uses Debris.idx*3, also for TALOS), Sigma_k = Covs[k]
-            const T *Kk = d.K + kn * NU * 9, *Sg = d.Sig + ((size_t)b * K1 + k) * 81;
+            const T *Sg = d.Sig + ((size_t)b * K1 + k) * 81;
             T KS[3][9];
             for (int r = 0; r < 3; ++r)
                 for (int j = 0; j < 9; ++j) {
                     T acc = T(0);
-                    for (int q = 0; q < 9; ++q) acc = fma(Kk[(3 * c + r) * 9 + q], Sg[q * 9 + j], acc);
+                    for (int q = 0; q < 9; ++q) acc = fma(em(d.K, (3 * c + r) * 9 + q), Sg[q * 9 + j], acc);
                     KS[r][j] = acc;
                 }
             for (int uu = 0; uu < 3; ++uu) {
                 T v = T(0);
-                for (int j = 0; j < 9; ++j) v = fma(KS[uu][j], Kk[(3 * c + uu) * 9 + j], v);
+                for (int j = 0; j < 9; ++j) v = fma(KS[uu][j], em(d.K, (3 * c + uu) * 9 + j), v);
                 const T sv = sqrt(v);
                 for (int r = 0; r < 4; ++r) {
                     const T g = cs[St::G + r * 3 + uu];
@@ -98,7 +109,7 @@ __global__ void __launch_bounds__(128) k_assemble(DevBuf<T> d, int only_active) 
             }
         }
         for (int r = 0; r < 4; ++r) cs[St::H + r] = h[r];
-        if (ROBOT == 1) {
+        if (FULL && ROBOT == 1) {
             // cop columns of B rows 6..8: -a dt [f]x R[:, 0:2];  tau column: a dt R[:, 2]
             const T *fc = uc + FO;
             const T sk[9] = {0, -fc[2], fc[1], fc[2], 0, -fc[0], -fc[1], fc[0], 0};
@@ -114,9 +125,13 @@ __global__ void __launch_bounds__(128) k_assemble(DevBuf<T> d, int only_active) 
     }
 }
 
-template __global__ void k_assemble<double, 0>(DevBuf<double>, int);
-template __global__ void k_assemble<double, 1>(DevBuf<double>, int);
-template __global__ void k_assemble<float, 0>(DevBuf<float>, int);
-template __global__ void k_assemble<float, 1>(DevBuf<float>, int);
+#define INST(T, R)                                                      \
+    template __global__ void k_assemble<T, R, true>(DevBuf<T>, int);  \
+    template __global__ void k_assemble<T, R, false>(DevBuf<T>, int);
+INST(double, 0)
+INST(double, 1)
+INST(float, 0)
+INST(float, 1)
+#undef INST
 
 }  // namespace cmpc

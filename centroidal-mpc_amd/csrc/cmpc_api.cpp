@@ -20,7 +20,7 @@ namespace cmpc {
 template <typename T, int R> __global__ void k_linearize(DevBuf<T>, int);
 template <typename T, int R> __global__ void k_lin_knots(DevBuf<T>, int);
 template <typename T, int R> __global__ void k_cov_scan(DevBuf<T>, int);
-template <typename T, int R> __global__ void k_assemble(DevBuf<T>, int);
+template <typename T, int R, bool FULL> __global__ void k_assemble(DevBuf<T>, int);
 template <typename T, int R> __global__ void k_qp_ipm(DevBuf<T>, int, int, T, T, T);
 template <typename T> __global__ void k_interpolate(DevBuf<T>, int, int, T *, T *);
 template <typename T, int R> __global__ void k_contact_plan(DevBuf<T>, const cmpc_gait *, const T *, uint8_t *, T *, T *);
@@ -99,19 +99,26 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
     if (B == 0) return;
     switch (phase) {
     case 0:
-        if (h->lin_lane) {   // one knot per lane (diagonal R), then the per-problem covariance scan
+        // one knot per lane (diagonal R; also writes the linearization part of the stage records),
+        // or one workgroup per problem (general R); then the per-problem covariance scan
+        if (h->lin_lane) {
             const long n = (long)B * h->N;
             hipLaunchKernelGGL((k_lin_knots<T, R>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream, d,
                                only_active);
-            hipLaunchKernelGGL((k_cov_scan<T, R>), dim3(B), dim3(64), 0, h->stream, d, only_active);
         } else {
             hipLaunchKernelGGL((k_linearize<T, R>), dim3(B), dim3(256), 0, h->stream, d, only_active);
         }
+        h->lin_lane_done = h->lin_lane;
+        hipLaunchKernelGGL((k_cov_scan<T, R>), dim3(B), dim3(64), 0, h->stream, d, only_active);
         break;
     case 1: {
         const long n = (long)B * (h->N + 1);
-        hipLaunchKernelGGL((k_assemble<T, R>), dim3((unsigned)((n + 127) / 128)), dim3(128), 0, h->stream, d,
-                           only_active);
+        if (h->lin_lane_done)
+            hipLaunchKernelGGL((k_assemble<T, R, false>), dim3((unsigned)((n + 127) / 128)), dim3(128), 0, h->stream, d,
+                               only_active);
+        else
+            hipLaunchKernelGGL((k_assemble<T, R, true>), dim3((unsigned)((n + 127) / 128)), dim3(128), 0, h->stream, d,
+                               only_active);
         break;
     }
     case 2: {
@@ -214,6 +221,23 @@ void reset_scp(cmpc_handle h, const int32_t *class_id) {
     }
     HIPCHK(hipMemcpyAsync(h->scp, st.data(), st.size() * sizeof(ScpState), hipMemcpyHostToDevice, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
+}
+
+// Knots [kn0, kn0 + n) of an element-major array (DevBuf::LS) into the knot-major host layout
+// dst[kn][e] (e < ne): one strided 2-D copy, transposed on the host.
+void dl_knots(cmpc_handle h, double *dst, const void *src, size_t kn0, size_t n, size_t ne) {
+    if (!dst || n == 0) return;
+    const size_t es = h->esz(), LS = (size_t)h->max_batch * h->N;
+    std::vector<unsigned char> tmp(n * ne * es);
+    HIPCHK(hipMemcpy2DAsync(tmp.data(), n * es, (const char *)src + kn0 * es, LS * es, n * es, ne,
+                            hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    for (size_t e = 0; e < ne; ++e)
+        for (size_t k = 0; k < n; ++k) {
+            const size_t i = e * n + k;
+            dst[k * ne + e] = es == 8 ? reinterpret_cast<const double *>(tmp.data())[i]
+                                      : double(reinterpret_cast<const float *>(tmp.data())[i]);
+        }
 }
 
 std::vector<ScpState> get_scp(cmpc_handle h) {
@@ -588,11 +612,11 @@ int cmpc_get_linearization(cmpc_handle h, double *f, double *A, double *Bu, doub
         auto dl = [&](double *dst, void *src, size_t n) {
             if (h->prec == CMPC_PREC_F64) from_dev<double>(h, dst, src, n); else from_dev<float>(h, dst, src, n);
         };
-        dl(f, h->f, B * N * 9);
-        dl(A, h->A, B * N * 81);
-        dl(Bu, h->Bu, B * N * 9 * NU);
-        dl(C, h->C, B * N * 9 * 3 * NC);
-        dl(K, h->K, B * N * NU * 9);
+        dl_knots(h, f, h->f, 0, B * N, 9);
+        dl_knots(h, A, h->A, 0, B * N, 81);
+        dl_knots(h, Bu, h->Bu, 0, B * N, 9 * NU);
+        dl_knots(h, C, h->C, 0, B * N, 9 * 3 * NC);
+        dl_knots(h, K, h->K, 0, B * N, NU * 9);
         dl(Sigma, h->Sig, B * (N + 1) * 81);
     });
 }
@@ -625,8 +649,10 @@ int cmpc_export_qp(cmpc_handle h, int b, double *P_x, int32_t *P_i, int32_t *P_p
         const int KP = KPC;
         dl(st, h->stage, (size_t)b * KP * SS, (size_t)KP * SS);
         auto sf = [&](int k, int f) { return st[(size_t)f * KP + k]; };   // field-major records
-        dl(A, h->A, (size_t)b * N * 81, (size_t)N * 81);
-        dl(Bm, h->Bu, (size_t)b * N * 9 * NU, (size_t)N * 9 * NU);
+        A.resize((size_t)N * 81);
+        Bm.resize((size_t)N * 9 * NU);
+        dl_knots(h, A.data(), h->A, (size_t)b * N, N, 81);
+        dl_knots(h, Bm.data(), h->Bu, (size_t)b * N, N, 9 * NU);
         dl(xb, h->Xbar, (size_t)b * K1 * 9, (size_t)K1 * 9);
         std::vector<int8_t> lg((size_t)N * NC);
         from_dev_raw(h, lg.data(), (char *)h->logic + (size_t)b * N * NC, lg.size());

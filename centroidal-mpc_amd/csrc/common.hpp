@@ -69,9 +69,13 @@ template <typename T> struct DevBuf {
     const T *Xbar, *Ubar;    // (B,N+1,9) (B,N,NU) warm start: tracking reference, boundary states
     T *Xlin, *Ulin;          // (B,N+1,9) (B,N,NU) linearization point (= warm start in reference mode)
     int scp_mode;            // CMPC_SCP_MODE_*
-    // linearization
-    T *f, *A, *Bu, *C, *K, *Sig;    // (B,N,9) (B,N,81) (B,N,108) (B,N,9*3NC) (B,N,108) (B,N+1,81)
-    T *Acl, *Qw;                    // scan helpers (B,N,81) x2
+    // linearization.  The per-knot arrays are element-major: element e of knot kn = b * N + k at
+    // X[e * LS + kn] (LS = max_batch * N), so the knot-per-lane kernels read and write them
+    // coalesced; the C ABI getters transpose to the knot-major layouts of include/cmpc.h.
+    T *f, *A, *Bu, *C, *K;          // elements 9 | 81 | 9 * NU | 9 * 3NC | NU * 9 (row-major per knot)
+    T *Sig;                         // (B, N+1, 81) knot-major (written by the scan, one wave per problem)
+    T *Acl, *Qw;                    // scan helpers, 81 elements each, element-major
+    size_t LS;
     // assembled stage records (B,N+1,SIZE) and per-problem cw = -1/omega
     T *stage;
     T *cw;

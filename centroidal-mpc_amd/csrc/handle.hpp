@@ -51,6 +51,7 @@ struct cmpc_handle_s {
          *Ulin = nullptr;
     int scp_mode = CMPC_SCP_MODE_REFERENCE;
     bool lin_lane = true;   // knot-per-lane linearization (diagonal R); else k_linearize
+    bool lin_lane_done = false;   // the last linearization came from k_lin_knots (stage partly written)
     // RCCL communicator of the batch split (comm.cpp); nullptr until cmpc_comm_init
     void *comm = nullptr;
     int comm_rank = 0, comm_size = 1;
@@ -74,6 +75,7 @@ struct cmpc_handle_s {
         d.Xlin = (T *)Xlin; d.Ulin = (T *)Ulin; d.scp_mode = scp_mode;
         d.f = (T *)f; d.A = (T *)A; d.Bu = (T *)Bu; d.C = (T *)C; d.K = (T *)K; d.Sig = (T *)Sig;
         d.Acl = (T *)Acl; d.Qw = (T *)Qw; d.stage = (T *)stage; d.cw = (T *)cw;
+        d.LS = (size_t)max_batch * N;
         d.xs = (T *)xs; d.us = (T *)us; d.ts = (T *)ts; d.nus = (T *)nus; d.lams = (T *)lams;
         d.qp_status = (int32_t *)qp_status; d.qp_iters = (int32_t *)qp_iters;
         d.qp_merit = (T *)qp_merit; d.qp_nref = (int32_t *)qp_nref;

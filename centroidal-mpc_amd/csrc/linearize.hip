@@ -8,8 +8,8 @@
 // elided here).
 //
 // Mapping: one workgroup (4 waves) per problem; each wave linearizes knots k = wave, wave+4, ...
-// with its small matrices staged in LDS (lanes over matrix entries); then wave 0 runs the
-// O(N) covariance scan for the problem.  Per knot: ~14 kflop (LQR) in LDS, ~3 KB of HBM
+// with its small matrices staged in LDS (lanes over matrix entries); k_cov_scan then runs the
+// O(N) covariance scan for the problem.  Used when R is not diagonal (k_lin_knots otherwise).  Per knot: ~14 kflop (LQR) in LDS, ~3 KB of HBM
 // traffic (inputs 0.6 KB, outputs f/A/B/C/K/Acl/Qw 2.6 KB at fp64).
 #include "common.hpp"
 
@@ -182,7 +182,7 @@ __device__ void linearize_knot(const DevBuf<T> &d, const DevParams<T> &prm, int 
                 F += s.a[c] * v;
             }
         }
-        d.f[kn * 9 + i] = s.x[i] + F * dt;
+        d.f[(size_t)i * d.LS + kn] = s.x[i] + F * dt;
     }
     // ---- A, B, C closed form (jacfwd at :230-232)
     for (int e = lane; e < 81; e += WAVE) {
@@ -197,7 +197,7 @@ __device__ void linearize_knot(const DevBuf<T> &d, const DevParams<T> &prm, int 
             v = dt * skew_at<T>(w, r, j);
         }
         s.A[e] = v;
-        d.A[kn * 81 + e] = v;
+        d.A[(size_t)e * d.LS + kn] = v;
     }
     for (int e = lane; e < 9 * NU; e += WAVE) {
         const int i = e / NU, j = e % NU, c = j / NUPC, q = j % NUPC;
@@ -228,7 +228,7 @@ __device__ void linearize_knot(const DevBuf<T> &d, const DevParams<T> &prm, int 
             }
         }
         s.Bm[e] = v;
-        d.Bu[kn * 9 * NU + e] = v;
+        d.Bu[(size_t)e * d.LS + kn] = v;
     }
     for (int e = lane; e < 9 * NW; e += WAVE) {
         const int i = e / NW, j = e % NW, c = j / 3, q = j % 3;
@@ -238,7 +238,7 @@ __device__ void linearize_knot(const DevBuf<T> &d, const DevParams<T> &prm, int 
             v = -dt * s.a[c] * skew_at<T>(f, i - 6, q);
         }
         s.Cm[e] = v;
-        d.C[kn * 9 * NW + e] = v;
+        d.C[(size_t)e * d.LS + kn] = v;
     }
     for (int e = lane; e < 81; e += WAVE) s.P[e] = prm.Q[e];
     wave_sync();
@@ -259,13 +259,13 @@ __device__ void linearize_knot(const DevBuf<T> &d, const DevParams<T> &prm, int 
             wave_sync();
         }
     }
-    for (int e = lane; e < NU * 9; e += WAVE) d.K[kn * NU * 9 + e] = -s.X[e];
+    for (int e = lane; e < NU * 9; e += WAVE) d.K[(size_t)e * d.LS + kn] = -s.X[e];
     // ---- scan helpers: Acl = A + B K, Qw = C W C' + eta
     for (int e = lane; e < 81; e += WAVE) {
         const int i = e / 9, j = e % 9;
         T acc = s.A[e];
         for (int q = 0; q < NU; ++q) acc -= s.Bm[i * NU + q] * s.X[q * 9 + j];
-        d.Acl[kn * 81 + e] = acc;
+        d.Acl[(size_t)e * d.LS + kn] = acc;
     }
     static_assert(9 * NW <= 9 * NU, "C W scratch");
     T *cw = s.PB;
@@ -280,17 +280,13 @@ __device__ void linearize_knot(const DevBuf<T> &d, const DevParams<T> &prm, int 
         const int i = e / 9, j = e % 9;
         T acc = prm.cov_eta[e];
         for (int q = 0; q < NW; ++q) acc = fma(cw[i * NW + q], s.Cm[j * NW + q], acc);
-        d.Qw[kn * 81 + e] = acc;
+        d.Qw[(size_t)e * d.LS + kn] = acc;
     }
     wave_sync();
 }
 
-// Covariance scan (src/centroidal_model.py:234-238, 266, 284), wave 0 of the workgroup after all
-// knots are linearized: Sigma_{k+1} = Acl_k Sigma_k Acl_k' + Qw_k.  The per-step blocks stream
-// through the (then dead) per-knot LDS scratch in double-buffered chunks of KS steps, each
-// chunk's loads issued a chunk ahead inside one loop iteration (no in-flight registers over the
-// back-edge), so the 100-step chain runs out of LDS.
-constexpr int KS = 4;
+// The general-R path (non-diagonal LQR weight): one workgroup (4 waves) per problem, one wave per
+// knot; the covariance scan then runs in k_cov_scan (linearize_lane.hip).
 template <typename T, int ROBOT>
 __global__ void __launch_bounds__(256, 4) k_linearize(DevBuf<T> d, int only_active) {
     const int b = blockIdx.x;
@@ -308,119 +304,10 @@ __global__ void __launch_bounds__(256, 4) k_linearize(DevBuf<T> d, int only_acti
 #ifdef CMPC_STAMPS
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
 #endif
-    __syncthreads();
-    __threadfence_block();
-    if (wid != 0) return;
-    constexpr int CH = 2 * KS * 81;                          // one chunk: KS Acl + KS Qw blocks
-    constexpr int PL = (CH + WAVE - 1) / WAVE;
-    static_assert(2 * CH * sizeof(T) <= 3 * sizeof(LinSmem<T, ROBOT>), "scan chunk buffers");
-    T *buf = reinterpret_cast<T *>(&sm[1]);
-    T *S = sm[0].P, *Tm = sm[0].AtP;
-    const T *Acl = d.Acl + (size_t)b * N * 81, *Qw = d.Qw + (size_t)b * N * 81;
-    T reg[PL];
-    auto issue = [&](int c) {
-#pragma unroll
-        for (int r = 0; r < PL; ++r) {
-            const int e = min(lane + r * WAVE, CH - 1), blk = e / 81, w = e % 81;
-            const int k = min(c * KS + blk % KS, N - 1);
-            reg[r] = (blk < KS ? Acl : Qw)[(size_t)k * 81 + w];
-        }
-    };
-    auto land = [&](int c) {
-        T *dst = buf + (c & 1) * CH;
-#pragma unroll
-        for (int r = 0; r < PL; ++r)
-            if (lane + r * WAVE < CH) dst[lane + r * WAVE] = reg[r];
-    };
-    for (int e = lane; e < 81; e += WAVE) {
-        S[e] = T(0);
-        d.Sig[((size_t)b * (N + 1)) * 81 + e] = T(0);
-    }
-    issue(0);
-    land(0);
-    wave_sync();
-    // fp64: Sigma stays in the matrix-core accumulator layout for the whole scan (C/D lane l,
-    // register r = Sigma[(l >> 4) + 4 r][l & 15]).  Y = Sigma Acl' takes Sigma as its A operand
-    // straight from those registers (Sigma is symmetric, so register kb holds A[l & 15][4 kb +
-    // (l >> 4)]); Sigma' = Acl Y + Qw takes Y as its B operand the same way (it sums over Y's
-    // row index).  Per step only Acl and Qw are read from LDS.
-    [[maybe_unused]] lin_v4d Sreg = {0.0, 0.0, 0.0, 0.0};
-    const int r16 = lane & 15, q4 = lane >> 4;
-    for (int c = 0; c * KS < N; ++c) {
-        issue(c + 1);
-        const T *cb = buf + (c & 1) * CH;
-        for (int q = 0; q < KS; ++q) {
-            const int k = c * KS + q;
-            if (k >= N) break;
-            const T *Ac = cb + q * 81, *Q = cb + (KS + q) * 81;
-            if constexpr (sizeof(T) == 8) {
-                double av[3];   // Acl[l & 15][4 kb + (l >> 4)] (zero outside 9 x 9)
-#pragma unroll
-                for (int kb = 0; kb < 3; ++kb) {
-                    const int m = 4 * kb + q4;
-                    av[kb] = (r16 < 9 && m < 9) ? Ac[(r16 < 9 ? r16 : 0) * 9 + (m < 9 ? m : 0)] : 0.0;
-                }
-                lin_v4d qw;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int i = q4 + 4 * r;
-                    qw[r] = (i < 9 && r16 < 9) ? Q[(i < 9 ? i : 0) * 9 + (r16 < 9 ? r16 : 0)] : 0.0;
-                }
-                lin_v4d Y = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-                for (int kb = 0; kb < 3; ++kb) Y = __builtin_amdgcn_mfma_f64_16x16x4f64(Sreg[kb], av[kb], Y, 0, 0, 0);
-                Sreg = qw;
-#pragma unroll
-                for (int kb = 0; kb < 3; ++kb) Sreg = __builtin_amdgcn_mfma_f64_16x16x4f64(av[kb], Y[kb], Sreg, 0, 0, 0);
-                T *so = d.Sig + ((size_t)b * (N + 1) + k + 1) * 81;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int i = q4 + 4 * r;
-                    if (i < 9 && r16 < 9) so[i * 9 + r16] = Sreg[r];
-                }
-                continue;
-            }
-            for (int e = lane; e < 81; e += WAVE) {     // Tm = Acl S
-                const int i = e / 9, j = e % 9;
-                T a[9], sv[9];
-#pragma unroll
-                for (int m = 0; m < 9; ++m) { a[m] = Ac[i * 9 + m]; sv[m] = S[m * 9 + j]; }
-                T acc = T(0);
-#pragma unroll
-                for (int m = 0; m < 9; ++m) acc = fma(a[m], sv[m], acc);
-                Tm[e] = acc;
-            }
-            wave_sync();
-            T out[2];
-#pragma unroll
-            for (int r = 0; r < 2; ++r) {   // Tm Acl' + Qw
-                const int e = min(lane + r * WAVE, 80), i = e / 9, j = e % 9;
-                T t[9], a[9];
-#pragma unroll
-                for (int m = 0; m < 9; ++m) { t[m] = Tm[i * 9 + m]; a[m] = Ac[j * 9 + m]; }
-                T acc = Q[e];
-#pragma unroll
-                for (int m = 0; m < 9; ++m) acc = fma(t[m], a[m], acc);
-                out[r] = acc;
-            }
-            wave_sync();
-#pragma unroll
-            for (int r = 0; r < 2; ++r) {
-                const int e = lane + r * WAVE;
-                if (e < 81) {
-                    S[e] = out[r];
-                    d.Sig[((size_t)b * (N + 1) + k + 1) * 81 + e] = out[r];
-                }
-            }
-            wave_sync();
-        }
-        land(c + 1);
-        wave_sync();
-    }
 #ifdef CMPC_STAMPS
     if (lane == 0) {
         d.stamps[(size_t)b * 16 + 9] = t1 - t0;
-        d.stamps[(size_t)b * 16 + 10] = __builtin_amdgcn_s_memtime() - t1;
+        d.stamps[(size_t)b * 16 + 10] = 0;
     }
 #endif
 }

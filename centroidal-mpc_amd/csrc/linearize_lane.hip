@@ -14,6 +14,13 @@
 // its block structure, never as a dense matrix.  The covariance scan itself (sequential over the
 // knots) runs in k_cov_scan, one wave per problem on the matrix cores.
 //
+// The kernel also writes the parts of the QP stage record that depend only on the linearization
+// (dynamics rhs r_k = A xbar + B ubar - f, the compact A and B data, the friction rows G), which
+// k_assemble computed from these arrays before; k_assemble<.., false> then adds the fields that
+// depend on the SCP state (trust-region bounds and weight, tracking gradient, chance back-off).
+// Outputs are element-major (DevBuf::LS): lane kn writes element e at e * LS + kn, so every store
+// of the wave is one contiguous 512-B (fp64) transaction.
+//
 // Non-diagonal R falls back to k_linearize (linearize.hip), which works with R + B'PB directly.
 #include "common.hpp"
 
@@ -151,10 +158,8 @@ __global__ void __launch_bounds__(256, 1) k_lin_knots(DevBuf<T> d, int only_acti
     for (int i = 0; i < NU; ++i) u[i] = us[i];
 #pragma unroll
     for (int i = 0; i < 3 * NC; ++i) p[i] = d.pos[kn * 3 * NC + i];
-    if (ROBOT == 1) {
 #pragma unroll
-        for (int i = 0; i < 9 * NC; ++i) rot[i] = d.rot[kn * 9 * NC + i];
-    }
+    for (int i = 0; i < 9 * NC; ++i) rot[i] = d.rot[kn * 9 * NC + i];
 #pragma unroll
     for (int c = 0; c < NC; ++c) a[c] = T(d.logic[kn * NC + c]);
     const T dt = prm.dt, m = prm.mass, beta = dt / m;
@@ -169,6 +174,10 @@ __global__ void __launch_bounds__(256, 1) k_lin_knots(DevBuf<T> d, int only_acti
             w[z] = fma(a[c], u[NUPC * c + FO + z], w[z]);
         }
     }
+    auto em = [&](T *base, int e) -> T & { return base[(size_t)e * d.LS + kn]; };
+    using St = Stage<ROBOT>;
+    const SV<T> st{d.stage + (size_t)b * St::SIZE * KPC + k};   // field-major stage record (common.hpp)
+    T fx[9];
     // ---- f = x + dt F(x, u)   (src/centroidal_model.py:189-212)
     {
         T F[9];
@@ -191,14 +200,15 @@ __global__ void __launch_bounds__(256, 1) k_lin_knots(DevBuf<T> d, int only_acti
                 F[6 + r] = fma(a[c], v, F[6 + r]);
             }
         }
-        T *fo = d.f + kn * 9;
 #pragma unroll
-        for (int i = 0; i < 9; ++i) fo[i] = x[i] + F[i] * dt;
+        for (int i = 0; i < 9; ++i) fx[i] = x[i] + F[i] * dt;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) em(d.f, i) = fx[i];
     }
     const T Wm[3][3] = {{T(0), -dt * w[2], dt * w[1]}, {dt * w[2], T(0), -dt * w[0]}, {-dt * w[1], dt * w[0], T(0)}};
     // ---- A, B, C (jacfwd at :230-232), closed form
+    // ---- A, B, C (jacfwd at :230-232) and the linearization part of the stage record
     {
-        T *Ao = d.A + kn * 81;
 #pragma unroll
         for (int i = 0; i < 9; ++i)
 #pragma unroll
@@ -206,9 +216,18 @@ __global__ void __launch_bounds__(256, 1) k_lin_knots(DevBuf<T> d, int only_acti
                 T v = (i == j) ? T(1) : T(0);
                 if (i < 3 && j == i + 3) v = beta;
                 if (i >= 6 && j < 3) v = Wm[i - 6][j];
-                Ao[i * 9 + j] = v;
+                em(d.A, i * 9 + j) = v;
             }
-        T *Bo = d.Bu + kn * 9 * NU, *Co = d.C + kn * 9 * NW;
+        // r_k = A xbar + B ubar - f (src/constraints.py:36-45)
+        T r[9];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) r[i] = fma(beta, x[3 + i], x[i]);
+#pragma unroll
+        for (int i = 3; i < 6; ++i) r[i] = x[i];
+#pragma unroll
+        for (int i = 6; i < 9; ++i) r[i] = x[i] + Wm[i - 6][0] * x[0] + Wm[i - 6][1] * x[1] + Wm[i - 6][2] * x[2];
+        const T ml = prm.mu / sqrt(T(2));
+        const T Fmu[4][3] = {{1, 0, -ml}, {-1, 0, -ml}, {0, 1, -ml}, {0, -1, -ml}};
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
             ContactB<T, ROBOT> Bc;
@@ -216,14 +235,41 @@ __global__ void __launch_bounds__(256, 1) k_lin_knots(DevBuf<T> d, int only_acti
 #pragma unroll
             for (int i = 0; i < 9; ++i)
 #pragma unroll
-                for (int q = 0; q < NUPC; ++q) Bo[i * NU + NUPC * c + q] = i < 3 ? T(0) : Bc.b[i - 3][q];
+                for (int q = 0; q < NUPC; ++q) em(d.Bu, i * NU + NUPC * c + q) = i < 3 ? T(0) : Bc.b[i - 3][q];
+#pragma unroll
+            for (int i = 0; i < 6; ++i)
+#pragma unroll
+                for (int q = 0; q < NUPC; ++q) r[3 + i] = fma(Bc.b[i][q], u[NUPC * c + q], r[3 + i]);
             const T *f = u + NUPC * c + FO;
             const T fs[3][3] = {{T(0), -f[2], f[1]}, {f[2], T(0), -f[0]}, {-f[1], f[0], T(0)}};
 #pragma unroll
             for (int i = 0; i < 9; ++i)
 #pragma unroll
-                for (int q = 0; q < 3; ++q) Co[i * NW + 3 * c + q] = i < 6 ? T(0) : -dt * a[c] * fs[i - 6][q];
+                for (int q = 0; q < 3; ++q) em(d.C, i * NW + 3 * c + q) = i < 6 ? T(0) : -dt * a[c] * fs[i - 6][q];
+            // per-contact stage fields: alpha, lever, friction rows (F_mu R')[0:4], TALOS cop / tau columns
+            const SV<T> cs = st + (St::CON + St::CS * c);
+            cs[St::ALPHA] = dt * a[c];
+#pragma unroll
+            for (int z = 0; z < 3; ++z) cs[St::LEVER + z] = lev[c][z];
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+                for (int q = 0; q < 3; ++q)
+                    cs[St::G + rr * 3 + q] = Fmu[rr][0] * rot[9 * c + q * 3] + Fmu[rr][1] * rot[9 * c + q * 3 + 1] +
+                                             Fmu[rr][2] * rot[9 * c + q * 3 + 2];
+            if (ROBOT == 1) {
+#pragma unroll
+                for (int rr = 0; rr < 3; ++rr) {
+                    cs[St::BCOP + rr * 2] = Bc.b[3 + rr][0];
+                    cs[St::BCOP + rr * 2 + 1] = Bc.b[3 + rr][1];
+                    cs[St::BTAU + rr] = Bc.b[3 + rr][5];
+                }
+            }
         }
+#pragma unroll
+        for (int i = 0; i < 9; ++i) st[St::R + i] = r[i] - fx[i];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) st[St::W + q] = dt * w[q];
     }
     // ---- G = B R^-1 B' (rows 3..8), R diagonal
     T G[21];   // packed lower 6x6
@@ -268,7 +314,6 @@ __global__ void __launch_bounds__(256, 1) k_lin_knots(DevBuf<T> d, int only_acti
 #pragma unroll
         for (int j = 0; j < 9; ++j) Y6[r][j] = MA_at(Ni, beta, Wm, 3 + r, j);
     {
-        T *Ko = d.K + kn * NU * 9;
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
             ContactB<T, ROBOT> Bc;
@@ -281,13 +326,12 @@ __global__ void __launch_bounds__(256, 1) k_lin_knots(DevBuf<T> d, int only_acti
                     T v = T(0);
 #pragma unroll
                     for (int r = 0; r < 6; ++r) v = fma(Bc.b[r][q], Y6[r][j], v);
-                    Ko[(NUPC * c + q) * 9 + j] = -ri * v;
+                    em(d.K, (NUPC * c + q) * 9 + j) = -ri * v;
                 }
             }
         }
     }
     {
-        T *Ao = d.Acl + kn * 81;
 #pragma unroll
         for (int i = 0; i < 9; ++i)
 #pragma unroll
@@ -303,7 +347,7 @@ __global__ void __launch_bounds__(256, 1) k_lin_knots(DevBuf<T> d, int only_acti
                         v = fma(-g, Y6[r][j], v);
                     }
                 }
-                Ao[i * 9 + j] = v;
+                em(d.Acl, i * 9 + j) = v;
             }
     }
     // ---- Qw = C W C' + eta (C: rows 6..8, -dt a_c [f_c]x)
@@ -328,7 +372,6 @@ __global__ void __launch_bounds__(256, 1) k_lin_knots(DevBuf<T> d, int only_acti
                 for (int q = 0; q < NW; ++q) v = fma(Cl[r][q], prm.cov_w[q * NW + j], v);
                 CW[r][j] = v;
             }
-        T *Qo = d.Qw + kn * 81;
 #pragma unroll
         for (int i = 0; i < 9; ++i)
 #pragma unroll
@@ -338,7 +381,7 @@ __global__ void __launch_bounds__(256, 1) k_lin_knots(DevBuf<T> d, int only_acti
 #pragma unroll
                     for (int q = 0; q < NW; ++q) v = fma(CW[i - 6][q], Cl[j - 6][q], v);
                 }
-                Qo[i * 9 + j] = v;
+                em(d.Qw, i * 9 + j) = v;
             }
     }
 }
@@ -358,14 +401,14 @@ template <typename T, int ROBOT> __global__ void __launch_bounds__(64, 4) k_cov_
     __shared__ T buf[2 * CH];
     __shared__ T S[81], Tm[81];
     const int lane = threadIdx.x, N = d.N;
-    const T *Acl = d.Acl + (size_t)b * N * 81, *Qw = d.Qw + (size_t)b * N * 81;
+    const T *Acl = d.Acl + (size_t)b * N, *Qw = d.Qw + (size_t)b * N;   // element-major (DevBuf::LS)
     T reg[PL];
     auto issue = [&](int c) {
 #pragma unroll
         for (int r = 0; r < PL; ++r) {
             const int e = min(lane + r * WAVE, CH - 1), blk = e / 81, w = e % 81;
             const int k = min(c * SKS + blk % SKS, N - 1);
-            reg[r] = (blk < SKS ? Acl : Qw)[(size_t)k * 81 + w];
+            reg[r] = (blk < SKS ? Acl : Qw)[(size_t)w * d.LS + k];
         }
     };
     auto land = [&](int c) {

@@ -189,13 +189,13 @@ __global__ void __launch_bounds__(ACC_NT) k_accept(DevBuf<T> d, int fixed_iters)
         }
         __syncthreads();
         for (int p = tid; p < nk * 9; p += ACC_NT) {
-            const int kk = p / 9, i = p % 9;
+            const int kk = p % nk, i = p / nk;   // neighbouring threads: neighbouring knots (element-major arrays)
             const size_t kn = (size_t)b * N + k0 + kk;
             const T *rec = acc_sm + kk * ACC_REC;
-            const T *Ar = d.A + kn * 81 + i * 9, *Br = d.Bu + kn * 9 * NU + i * NU;
-            T lin = d.f[kn * 9 + i];
-            for (int j = 0; j < 9; ++j) lin = fma(Ar[j], rec[9 + j], lin);
-            for (int j = 0; j < NU; ++j) lin = fma(Br[j], rec[18 + j], lin);
+            const T *Ar = d.A + (size_t)(i * 9) * d.LS + kn, *Br = d.Bu + (size_t)(i * NU) * d.LS + kn;
+            T lin = d.f[(size_t)i * d.LS + kn];
+            for (int j = 0; j < 9; ++j) lin = fma(Ar[(size_t)j * d.LS], rec[9 + j], lin);
+            for (int j = 0; j < NU; ++j) lin = fma(Br[(size_t)j * d.LS], rec[18 + j], lin);
             if (i >= 6) acc[0] += sq(rec[i] - lin);
             acc[1] += lin * lin;
         }
@@ -265,7 +265,10 @@ __global__ void __launch_bounds__(ACC_NT) k_accept(DevBuf<T> d, int fixed_iters)
     // accepted: keep X, U and this iteration's LQR gains / covariances
     for (int e = tid; e < K1 * 9; e += ACC_NT) d.Xacc[(size_t)b * K1 * 9 + e] = Xs[e];
     for (int e = tid; e < N * NU; e += ACC_NT) d.Uacc[(size_t)b * N * NU + e] = Us[e];
-    for (int e = tid; e < N * NU * 9; e += ACC_NT) d.Kacc[(size_t)b * N * NU * 9 + e] = d.K[(size_t)b * N * NU * 9 + e];
+    for (int e = tid; e < N * NU * 9; e += ACC_NT) {   // element-major K -> the knot-major accepted copy
+        const int q = e / N, k = e % N;
+        d.Kacc[((size_t)b * N + k) * NU * 9 + q] = d.K[(size_t)q * d.LS + (size_t)b * N + k];
+    }
     for (int e = tid; e < K1 * 81; e += ACC_NT) d.Sacc[(size_t)b * K1 * 81 + e] = d.Sig[(size_t)b * K1 * 81 + e];
     if (d.scp_mode == CMPC_SCP_MODE_GUSTO) {   // the accepted solution becomes the linearization point
         for (int e = tid; e < K1 * 9; e += ACC_NT) Xb[e] = Xs[e];
