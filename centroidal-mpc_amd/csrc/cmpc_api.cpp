@@ -27,6 +27,7 @@ template <typename T, int R> __global__ void k_contact_plan(DevBuf<T>, const cmp
 template <typename T, int R> __global__ void k_default_controls(DevBuf<T>, T *);
 size_t ipm_lds_bytes(int N, int prec_bytes);
 template <typename T, int R> __global__ void k_accept(DevBuf<T>, int);
+template <typename T> __global__ void k_keep_accepted(DevBuf<T>);
 template <typename T, int R> __global__ void k_rollout(DevBuf<T>, const T *, const T *, T *);
 size_t ipm_workspace_elems(int N, int robot);
 }  // namespace cmpc
@@ -133,6 +134,11 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
     }
     case 3:
         hipLaunchKernelGGL((k_accept<T, R>), dim3(B), dim3(64), 0, h->stream, d, only_active ? 0 : 1);   // ACC_NT
+        {
+            const int per = (h->N + 1) * 90 + h->N * NU * 10;   // X, Sigma | U, K elements per problem
+            hipLaunchKernelGGL((k_keep_accepted<T>), dim3((unsigned)std::min(16, (per + 255) / 256), B), dim3(256), 0,
+                               h->stream, d);
+        }
         break;
     }
     HIPCHK(hipGetLastError());
@@ -807,7 +813,7 @@ int cmpc_get_solution(cmpc_handle h, double *X, double *U, double *K, double *Si
         };
         dl(X, h->Xacc, B * K1 * 9);
         dl(U, h->Uacc, B * N * NU);
-        dl(K, h->Kacc, B * N * NU * 9);
+        dl_knots(h, K, h->Kacc, 0, B * N, NU * 9);
         dl(Sigma, h->Sacc, B * K1 * 81);
         auto st = get_scp(h);
         for (size_t b = 0; b < B; ++b) {

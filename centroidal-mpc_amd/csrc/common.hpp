@@ -57,6 +57,7 @@ struct ScpState {
     int iter, status, success, n_accepted;
     int qp_status, qp_iters, decision, active;
     double conv;   // convergence measure of the last accepted iteration (GuSTO mode)
+    int keep, pad;   // this iteration was accepted: k_keep_accepted copies its solution/gains
 };
 
 // Device buffers of one handle.
@@ -92,7 +93,7 @@ template <typename T> struct DevBuf {
     // SCP
     ScpState *scp;
     unsigned long long *stamps;     // (B,16) per-phase cycle counters (diagnostic builds only)
-    T *Xacc, *Uacc, *Kacc, *Sacc;   // accepted solution (B,N+1,9) (B,N,NU) (B,N,108) (B,N+1,81)
+    T *Xacc, *Uacc, *Kacc, *Sacc;   // accepted solution (B,N+1,9) (B,N,NU) (108,LS) (B,N+1,81)
 };
 
 // ---------------------------------------------------------------- knot-minor layouts

@@ -15,113 +15,92 @@ namespace cmpc {
 
 enum { DEC_NONE = 0, DEC_ACCEPT = 1, DEC_REJECT_RHO = 2, DEC_REJECT_TR = 3, DEC_QP_FAILED = -1 };
 
-// Largest eigenvalue of the symmetric n x n matrix a (row-major, in LDS: rotations index it at run
-// time, which would put a private array in scratch memory), cyclic Jacobi on one thread.
-template <int n> __device__ double jacobi_lambda_max(double *a_) {
-    auto a = [&](int i, int j) -> double & { return a_[i * n + j]; };
-    for (int sweep = 0; sweep < 40; ++sweep) {
-        double off = 0.0, tot = 0.0;
-        for (int i = 0; i < n; ++i)
-            for (int j = 0; j < n; ++j) {
-                tot += a(i, j) * a(i, j);
-                if (i != j) off += a(i, j) * a(i, j);
-            }
-        if (off <= 1e-30 * tot || off == 0.0) break;
-        for (int p = 0; p < n - 1; ++p)
-            for (int q = p + 1; q < n; ++q) {
-                const double apq = a(p, q);
-                if (apq == 0.0) continue;
-                const double theta = (a(q, q) - a(p, p)) / (2.0 * apq);
-                const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-                const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
-                for (int k = 0; k < n; ++k) {
-                    const double akp = a(k, p), akq = a(k, q);
-                    a(k, p) = c * akp - s * akq;
-                    a(k, q) = s * akp + c * akq;
-                }
-                for (int k = 0; k < n; ++k) {
-                    const double apk = a(p, k), aqk = a(q, k);
-                    a(p, k) = c * apk - s * aqk;
-                    a(q, k) = s * apk + c * aqk;
-                }
-            }
+// Largest eigenvalue of the symmetric positive semidefinite n x n matrix g (row-major, in LDS) by
+// multisection on the wave: lane l tests the shift s_l = lo + (l + 1) (hi - lo) / 65 for
+// s_l I - g positive definite (LDL' pivots all positive, i.e. s_l > lambda_max, Sylvester's
+// inertia), and the lowest passing lane brackets lambda_max 65x tighter per round.  Start
+// bracket: max diagonal <= lambda_max <= Gershgorin bound.  Every lane runs the same rounds on
+// the same values, so the result is wave-uniform and deterministic; error ~ n eps ||g|| (the
+// backward error of the LDL' inertia), like a converged Jacobi sweep.  Must be called by a
+// whole 64-lane wave.
+template <int n> __device__ double lambda_max_psd(const double *g) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    double lo = 0.0, hi = 0.0;
+    for (int i = 0; i < n; ++i) {
+        double r = 0.0;
+        for (int j = 0; j < n; ++j) r += fabs(g[i * n + j]);
+        lo = fmax(lo, g[i * n + i]);
+        hi = fmax(hi, r);
     }
-    double m = a(0, 0);
-    for (int i = 1; i < n; ++i) m = fmax(m, a(i, i));
-    return m;
-}
-
-// The same in registers for small n: every rotation loop unrolled so all indices are constants
-// (the matrix lives in VGPRs; LDS or scratch put a ~100-cycle access in every dependent step)
-template <int n> __device__ double jacobi_lambda_max_reg(const double *g) {
-    double a[n][n];
-#pragma unroll
-    for (int i = 0; i < n; ++i)
-#pragma unroll
-        for (int j = 0; j < n; ++j) a[i][j] = g[i * n + j];
-    for (int sweep = 0; sweep < 40; ++sweep) {
-        double off = 0.0, tot = 0.0;
+    hi *= 1.0 + 4.0 * n * 2.3e-16;   // Gershgorin, rounded up
+    for (int round = 0; round < 16 && hi - lo > 2.3e-16 * hi; ++round) {
+        const double w = hi - lo;
+        const double s = lo + w * (double(lane + 1) / 65.0);
+        double c[n * (n + 1) / 2];   // upper triangle of s I - g, row-packed, eliminated in place
+        auto at = [](int i, int j) { return i * n - i * (i - 1) / 2 + (j - i); };
 #pragma unroll
         for (int i = 0; i < n; ++i)
 #pragma unroll
-            for (int j = 0; j < n; ++j) {
-                tot += a[i][j] * a[i][j];
-                if (i != j) off += a[i][j] * a[i][j];
+            for (int j = i; j < n; ++j) c[at(i, j)] = (i == j ? s : 0.0) - g[i * n + j];
+        bool pd = true;
+#pragma unroll
+        for (int k = 0; k < n; ++k) {
+            const double piv = c[at(k, k)];
+            pd = pd && piv > 0.0;
+            const double inv = 1.0 / piv;
+#pragma unroll
+            for (int i = k + 1; i < n; ++i) {
+                const double f = c[at(k, i)] * inv;
+#pragma unroll
+                for (int j = i; j < n; ++j) c[at(i, j)] = fma(-f, c[at(k, j)], c[at(i, j)]);
             }
-        if (off <= 1e-30 * tot || off == 0.0) break;
-#pragma unroll
-        for (int p = 0; p < n - 1; ++p)
-#pragma unroll
-            for (int q = p + 1; q < n; ++q) {
-                const double apq = a[p][q];
-                // apq == 0: identity rotation (c = 1, s = 0), kept branch-free
-                const double theta = (a[q][q] - a[p][p]) / (2.0 * (apq != 0.0 ? apq : 1.0));
-                const double t0 = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-                const double t = apq != 0.0 ? t0 : 0.0;
-                const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
-#pragma unroll
-                for (int k = 0; k < n; ++k) {
-                    const double akp = a[k][p], akq = a[k][q];
-                    a[k][p] = c * akp - s * akq;
-                    a[k][q] = s * akp + c * akq;
-                }
-#pragma unroll
-                for (int k = 0; k < n; ++k) {
-                    const double apk = a[p][k], aqk = a[q][k];
-                    a[p][k] = c * apk - s * aqk;
-                    a[q][k] = s * apk + c * aqk;
-                }
-            }
+        }
+        const unsigned long long m = __ballot(pd);
+        if (m == 0) {
+            lo = lo + w * (64.0 / 65.0);
+        } else {
+            const int l = __ffsll((long long)m) - 1;
+            hi = lo + w * (double(l + 1) / 65.0);
+            if (l > 0) lo = lo + w * (double(l) / 65.0);
+        }
     }
-    double m = a[0][0];
-#pragma unroll
-    for (int i = 1; i < n; ++i) m = fmax(m, a[i][i]);
-    return m;
+    return 0.5 * (lo + hi);
 }
 
 // Spectral norm of the (rows x cols) matrix V[c][r] - W[c][r] (W may be null): sqrt of the largest
-// eigenvalue of the rows x rows Gram matrix, accumulated over the workgroup (Gram entry per
-// thread), Jacobi on thread 0.  All threads receive the value.
+// eigenvalue of the rows x rows Gram matrix.  Columns go through LDS in chunks of SN_CC (one
+// coalesced pass over the contiguous V, W), each thread accumulates its Gram entries in column
+// order; eigenvalue by multisection on the (single-wave) workgroup.
+constexpr int SN_CC = 256;
 template <int rows, typename T>
-__device__ double spec_norm(const T *V, const T *W, int cols, double *gram, double *res) {
+__device__ double spec_norm(const T *V, const T *W, int cols, double *gram, double *buf /* rows * SN_CC */) {
+    constexpr int PER = (rows * rows + WAVE - 1) / WAVE;
     const int tid = threadIdx.x;
-    for (int e = tid; e < rows * rows; e += blockDim.x) {
-        const int i = e / rows, j = e % rows;
-        double g = 0.0;
-        for (int c = 0; c < cols; ++c) {
-            const double vi = double(V[(size_t)c * rows + i]) - (W ? double(W[(size_t)c * rows + i]) : 0.0);
-            const double vj = double(V[(size_t)c * rows + j]) - (W ? double(W[(size_t)c * rows + j]) : 0.0);
-            g += vi * vj;
+    double g[PER];
+#pragma unroll
+    for (int p = 0; p < PER; ++p) g[p] = 0.0;
+    for (int c0 = 0; c0 < cols; c0 += SN_CC) {
+        const int nc = min(SN_CC, cols - c0);
+        const T *v = V + (size_t)c0 * rows, *w = W ? W + (size_t)c0 * rows : nullptr;
+        for (int e = tid; e < nc * rows; e += WAVE) buf[e] = double(v[e]) - (w ? double(w[e]) : 0.0);
+        __syncthreads();
+#pragma unroll
+        for (int p = 0; p < PER; ++p) {
+            const int e = tid + p * WAVE;
+            if (e < rows * rows) {
+                const int i = e / rows, j = e % rows;
+                for (int c = 0; c < nc; ++c) g[p] = fma(buf[c * rows + i], buf[c * rows + j], g[p]);
+            }
         }
-        gram[e] = g;
+        __syncthreads();
     }
+#pragma unroll
+    for (int p = 0; p < PER; ++p)
+        if (tid + p * WAVE < rows * rows) gram[tid + p * WAVE] = g[p];
     __syncthreads();
-    if (tid == 0) {
-        if constexpr (rows <= 9) *res = sqrt(fmax(jacobi_lambda_max_reg<rows>(gram), 0.0));
-        else *res = sqrt(fmax(jacobi_lambda_max<rows>(gram), 0.0));   // in place (LDS)
-    }
-    __syncthreads();
-    return *res;
+    const double v = sqrt(fmax(lambda_max_psd<rows>(gram), 0.0));
+    __syncthreads();   // gram is reused by the next call
+    return v;
 }
 
 // x+ = x + dt F(x, u) for the knot-k contact data (integrate_model_one_step)
@@ -161,11 +140,15 @@ __global__ void __launch_bounds__(ACC_NT) k_accept(DevBuf<T> d, int fixed_iters)
     const int b = blockIdx.x;
     if (b >= d.B) return;
     ScpState &sc = d.scp[b];
-    if (!sc.active) return;
+    if (!sc.active) {
+        if (threadIdx.x == 0) sc.keep = 0;
+        return;
+    }
     __shared__ T red[2 * 4];
-    __shared__ double gram[NU * NU], nres[4];
-    __shared__ T acc_sm[ACC_KC * ACC_REC];
-    __shared__ int dec_sh;
+    __shared__ double gram[NU * NU];
+    __shared__ double smem[ACC_KC * ACC_REC];   // rho records, then spectral-norm column chunks
+    static_assert(NU * SN_CC <= ACC_KC * ACC_REC, "LDS");
+    T *acc_sm = reinterpret_cast<T *>(smem);
     const int tid = threadIdx.x, N = d.N, K1 = N + 1;
     const DevParams<T> &prm = d.params[d.class_id[b]];
     const T *Xs = d.xs + (size_t)b * K1 * 9, *Us = d.us + (size_t)b * N * NU;
@@ -204,14 +187,14 @@ __global__ void __launch_bounds__(ACC_NT) k_accept(DevBuf<T> d, int fixed_iters)
     block_reduce<T, ACC_NT, 2, 0>(acc, red);
     const double rho = double(acc[0]) / double(acc[1]);
     // ---- spectral norm of X_sol - X_prev (quirk Q6)
-    const double tr = spec_norm<9>(Xs, Xb, K1, gram, &nres[0]);
+    const double tr = spec_norm<9>(Xs, Xb, K1, gram, smem);
     // ---- GuSTO mode: convergence(sol, lin) = |dU|_2 / |U|_2 + |dX|_2 / |X|_2 (src/scp_solver.py:51-56),
     // needed only when this iteration is accepted (evaluated for every problem, cheap)
     double conv = 0.0;
     if (d.scp_mode == CMPC_SCP_MODE_GUSTO) {
-        const double nx = spec_norm<9>(Xs, (const T *)nullptr, K1, gram, &nres[1]);
-        const double nu_d = spec_norm<NU>(Us, Ub, N, gram, &nres[2]);
-        const double nu_n = spec_norm<NU>(Us, (const T *)nullptr, N, gram, &nres[3]);
+        const double nx = spec_norm<9>(Xs, (const T *)nullptr, K1, gram, smem);
+        const double nu_d = spec_norm<NU>(Us, Ub, N, gram, smem);
+        const double nu_n = spec_norm<NU>(Us, (const T *)nullptr, N, gram, smem);
         conv = nu_d / nu_n + tr / nx;
     }
     if (tid == 0) {
@@ -258,21 +241,38 @@ __global__ void __launch_bounds__(ACC_NT) k_accept(DevBuf<T> d, int fixed_iters)
             if (dec == DEC_ACCEPT) sc.conv = conv;
             if (sc.status == CMPC_SCP_RUNNING && sc.success) sc.status = CMPC_SCP_CONVERGED;
         }
-        dec_sh = dec;
+        sc.keep = dec == DEC_ACCEPT;
     }
-    __syncthreads();
-    if (dec_sh != DEC_ACCEPT) return;
-    // accepted: keep X, U and this iteration's LQR gains / covariances
-    for (int e = tid; e < K1 * 9; e += ACC_NT) d.Xacc[(size_t)b * K1 * 9 + e] = Xs[e];
-    for (int e = tid; e < N * NU; e += ACC_NT) d.Uacc[(size_t)b * N * NU + e] = Us[e];
-    for (int e = tid; e < N * NU * 9; e += ACC_NT) {   // element-major K -> the knot-major accepted copy
-        const int q = e / N, k = e % N;
-        d.Kacc[((size_t)b * N + k) * NU * 9 + q] = d.K[(size_t)q * d.LS + (size_t)b * N + k];
-    }
-    for (int e = tid; e < K1 * 81; e += ACC_NT) d.Sacc[(size_t)b * K1 * 81 + e] = d.Sig[(size_t)b * K1 * 81 + e];
-    if (d.scp_mode == CMPC_SCP_MODE_GUSTO) {   // the accepted solution becomes the linearization point
-        for (int e = tid; e < K1 * 9; e += ACC_NT) Xb[e] = Xs[e];
-        for (int e = tid; e < N * NU; e += ACC_NT) Ub[e] = Us[e];
+}
+
+// Accepted iterations keep X, U and this iteration's LQR gains / covariances (and, GuSTO mode,
+// become the linearization point): a grid over (element chunk, problem), so the ~170 KB per
+// accepted problem stream at HBM rate (one wave per problem copying them latency-bound took
+// ~200 us per SCP iteration at batch 1024, N = 100).
+template <typename T>
+__global__ void __launch_bounds__(256) k_keep_accepted(DevBuf<T> d) {
+    const int b = blockIdx.y;
+    if (b >= d.B || !d.scp[b].keep) return;
+    const int N = d.N, K1 = N + 1;
+    const int nx = K1 * 9, nu = N * NU, nk = N * NU * 9, ns = K1 * 81;
+    const bool gusto = d.scp_mode == CMPC_SCP_MODE_GUSTO;
+    const T *Xs = d.xs + (size_t)b * nx, *Us = d.us + (size_t)b * nu;
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < nx + nu + nk + ns; e += gridDim.x * 256) {
+        if (e < nx) {
+            d.Xacc[(size_t)b * nx + e] = Xs[e];
+            if (gusto) d.Xlin[(size_t)b * nx + e] = Xs[e];
+        } else if (e < nx + nu) {
+            const int i = e - nx;
+            d.Uacc[(size_t)b * nu + i] = Us[i];
+            if (gusto) d.Ulin[(size_t)b * nu + i] = Us[i];
+        } else if (e < nx + nu + nk) {   // element-major, like K
+            const int i = e - nx - nu;
+            const size_t j = (size_t)(i / N) * d.LS + (size_t)b * N + i % N;
+            d.Kacc[j] = d.K[j];
+        } else {
+            const size_t j = (size_t)b * ns + (e - nx - nu - nk);
+            d.Sacc[j] = d.Sig[j];
+        }
     }
 }
 
@@ -323,6 +323,8 @@ template __global__ void k_rollout<double, 1>(DevBuf<double>, const double *, co
 template __global__ void k_rollout<float, 0>(DevBuf<float>, const float *, const float *, float *);
 template __global__ void k_rollout<float, 1>(DevBuf<float>, const float *, const float *, float *);
 
+template __global__ void k_keep_accepted<double>(DevBuf<double>);
+template __global__ void k_keep_accepted<float>(DevBuf<float>);
 template __global__ void k_accept<double, 0>(DevBuf<double>, int);
 template __global__ void k_accept<double, 1>(DevBuf<double>, int);
 template __global__ void k_accept<float, 0>(DevBuf<float>, int);
