@@ -1811,12 +1811,17 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_update(const C
 
 // initialization step: full Newton step for z and nu; s = h - gz at the new z; lambda += dlambda.
 // vmax receives (max -s, max -lambda) over this knot's rows.
-// s = h - g'z at the new z for the present rows (absent rows keep s = 1: their affine step is
-// zero), branch-free with each row group's loads batched; restrict-qualified field pointers
+// Starting point after the initialization step: s = h - g'z at the new z for the present rows
+// (absent rows keep s = 1, lambda = 0: their affine step is zero).  Solo12: s and lambda floored
+// row by row at QP_INIT_FLOOR.  TALOS: vmax collects the largest violations for CVXOPT's shift of
+// every row (phase_init_shift).  On Solo12 the shift starts at mu ~ 700, far from the central
+// path (trot N=100: 9.3 Newton steps on average, 5.3 with the floors); on TALOS the floors were
+// not robust (oracle/ipm_mirror.py).  Branch-free with each row group's loads batched.
+#define QP_INIT_FLOOR 0.1
 template <typename T, int ROBOT>
 __device__ __forceinline__ void init_s_knot(const Ctx<T, ROBOT> &C, int k, T (&vmax)[2], const T *__restrict__ stp,
                                             const T *__restrict__ xs, const T *__restrict__ us,
-                                            const T *__restrict__ ts, T *__restrict__ ss, const T *__restrict__ ls) {
+                                            const T *__restrict__ ts, T *__restrict__ ss, T *__restrict__ ls) {
     using S = Stage<ROBOT>;
     using R_ = Rows<ROBOT>;
     constexpr int NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
@@ -1829,9 +1834,15 @@ __device__ __forceinline__ void init_s_knot(const Ctx<T, ROBOT> &C, int k, T (&v
     for (int i = 0; i < NU; ++i) u[i] = us[i * ld];   // k = N: padding column (unused)
     const T t = ts[0];
     auto put = [&](int r, bool pr, T v) {   // v = g'z - h
-        ss[r * ld] = pr ? -v : T(1);
-        vmax[0] = fmax(vmax[0], pr ? v : T(-1e300));
-        vmax[1] = fmax(vmax[1], pr ? -ls[r * ld] : T(-1e300));
+        const T l = ls[r * ld];
+        if (ROBOT == 0) {
+            ss[r * ld] = pr ? fmax(-v, T(QP_INIT_FLOOR)) : T(1);
+            ls[r * ld] = pr ? fmax(l, T(QP_INIT_FLOOR)) : l;
+        } else {
+            ss[r * ld] = pr ? -v : T(1);
+            vmax[0] = fmax(vmax[0], pr ? v : T(-1e300));
+            vmax[1] = fmax(vmax[1], pr ? -l : T(-1e300));
+        }
     };
 #pragma unroll
     for (int j = 0; j < 8; ++j)
@@ -1982,9 +1993,9 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
     __syncthreads();
     int status = CMPC_QP_MAX_ITER, it = 0, stall = 0, n_refine = 0;
     T mu_prev = T(-1), merit = T(0), prim_prev = T(0);
-    // it == 0 is the initialization step (CVXOPT-style): one full Newton step from
-    // s = lambda = 1 gives an equality-feasible least-squares start; s and lambda are then
-    // shifted by (1 + max violation) where negative.
+    // it == 0 is the initialization step: one full Newton step from s = lambda = 1 gives an
+    // equality-feasible least-squares start; s and lambda are then floored row by row (Solo12)
+    // or shifted by 1 + the largest violation (TALOS), see init_s_knot.
     for (it = 0; it <= max_iter; ++it) {
         const bool init = (it == 0);
         Norms<T, ROBOT> nm{0, 0, 0, 0, 0, 0, 0, 0};
@@ -2087,10 +2098,12 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
         if (init) {
             T vmax[2] = {T(-1e300), T(-1e300)};
             for (int k = tid; k < K1; k += NT) phase_init_step<T, ROBOT>(C, k, vmax);
-            block_reduce<T, NT, 2, 1>(vmax, red);
-            const T sh_s = vmax[0] >= T(0) ? T(1) + vmax[0] : T(0);
-            const T sh_l = vmax[1] >= T(0) ? T(1) + vmax[1] : T(0);
-            for (int k = tid; k < K1; k += NT) phase_init_shift<T, ROBOT>(C, k, sh_s, sh_l);
+            if (ROBOT == 1) {   // CVXOPT shift (Solo12 floors inside init_s_knot)
+                block_reduce<T, NT, 2, 1>(vmax, red);
+                const T sh_s = vmax[0] >= T(0) ? T(1) + vmax[0] : T(0);
+                const T sh_l = vmax[1] >= T(0) ? T(1) + vmax[1] : T(0);
+                for (int k = tid; k < K1; k += NT) phase_init_shift<T, ROBOT>(C, k, sh_s, sh_l);
+            }
             __syncthreads();
             continue;
         }

