@@ -39,7 +39,8 @@ class Params(ctypes.Structure):
 
 class QPSettings(ctypes.Structure):
     _fields_ = [('max_iter', ctypes.c_int32), ('eps_abs', ctypes.c_double), ('eps_rel', ctypes.c_double),
-                ('step_fraction', ctypes.c_double)]
+                ('step_fraction', ctypes.c_double), ('init_floor_s', ctypes.c_double),
+                ('init_floor_l', ctypes.c_double)]
 
 
 class Gait(ctypes.Structure):
@@ -210,13 +211,16 @@ class Solver:
         self.close()
 
     # ---- setup
-    def set_qp_settings(self, max_iter=None, eps_abs=None, eps_rel=None, step_fraction=None):
+    def set_qp_settings(self, max_iter=None, eps_abs=None, eps_rel=None, step_fraction=None, init_floor_s=None,
+                        init_floor_l=None):
         s = QPSettings()
         self.lib.cmpc_default_qp_settings(self.prec, ctypes.byref(s))
         if max_iter is not None: s.max_iter = int(max_iter)
         if eps_abs is not None: s.eps_abs = float(eps_abs)
         if eps_rel is not None: s.eps_rel = float(eps_rel)
         if step_fraction is not None: s.step_fraction = float(step_fraction)
+        if init_floor_s is not None: s.init_floor_s = float(init_floor_s)
+        if init_floor_l is not None: s.init_floor_l = float(init_floor_l)
         self._chk(self.lib.cmpc_set_qp_settings(self.h, ctypes.byref(s)), 'cmpc_set_qp_settings')
 
     def set_params(self, params):

@@ -21,7 +21,7 @@ template <typename T, int R> __global__ void k_linearize(DevBuf<T>, int);
 template <typename T, int R> __global__ void k_lin_knots(DevBuf<T>, int);
 template <typename T, int R> __global__ void k_cov_scan(DevBuf<T>, int);
 template <typename T, int R, bool FULL> __global__ void k_assemble(DevBuf<T>, int);
-template <typename T, int R> __global__ void k_qp_ipm(DevBuf<T>, int, int, T, T, T);
+template <typename T, int R> __global__ void k_qp_ipm(DevBuf<T>, int, int, T, T, T, T, T);
 template <typename T> __global__ void k_interpolate(DevBuf<T>, int, int, T *, T *);
 template <typename T, int R> __global__ void k_contact_plan(DevBuf<T>, const cmpc_gait *, const T *, uint8_t *, T *, T *);
 template <typename T, int R> __global__ void k_default_controls(DevBuf<T>, T *);
@@ -129,7 +129,8 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
         HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_qp_ipm<T, R>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         hipLaunchKernelGGL((k_qp_ipm<T, R>), dim3(B), dim3(IPM_NT), lds, h->stream, d, only_active, h->qs.max_iter,
-                           T(h->qs.eps_abs), T(h->qs.eps_rel), T(h->qs.step_fraction));
+                           T(h->qs.eps_abs), T(h->qs.eps_rel), T(h->qs.step_fraction), T(h->qs.init_floor_s),
+                           T(h->qs.init_floor_l));
         break;
     }
     case 3:
@@ -266,6 +267,8 @@ int cmpc_default_qp_settings(int precision, cmpc_qp_settings *s) {
     s->eps_abs = precision == CMPC_PREC_F64 ? 1e-10 : 1e-6;
     s->eps_rel = precision == CMPC_PREC_F64 ? 1e-10 : 1e-6;
     s->step_fraction = 0.99;
+    s->init_floor_s = 0.1;
+    s->init_floor_l = 0.1;
     return 0;
 }
 
@@ -352,7 +355,8 @@ int cmpc_destroy(cmpc_handle h) {
 
 int cmpc_set_qp_settings(cmpc_handle h, const cmpc_qp_settings *s) {
     return guard(h, [&] {
-        need(s && s->max_iter > 0 && s->step_fraction > 0 && s->step_fraction < 1, "invalid QP settings");
+        need(s && s->max_iter > 0 && s->step_fraction > 0 && s->step_fraction < 1 && s->init_floor_s >= 0 &&
+                 s->init_floor_l >= 0 && (s->init_floor_s > 0) == (s->init_floor_l > 0), "invalid QP settings");
         h->qs = *s;
     });
 }

@@ -146,6 +146,7 @@ template <typename T, int ROBOT> struct Ctx {
     T *Sd, *So;           // Schur diagonal blocks / inverses and couplings (workspace, see tw_factor_ends)
     LdsT<T> *vb;          // Schur rhs -> direction dnu, (N+2) x 9 block vector in LDS
     T dcap;               // cap on D = lambda/s for the CoP rows (D-form, folded into W_cop)
+    T fls, fll;           // Solo12 starting-point floors of s, lambda (0: CVXOPT shift)
     const LdsT<T> *wt;    // LDS copy of the cost weights: Wx | 1/Wx | Wu | 1/Wu (parameter loads
                           // next to workspace stores were each waited on alone)
     __device__ T Wx(int i) const { return wt[i]; }
@@ -241,8 +242,9 @@ __device__ __forceinline__ int p4(int i, int j) { if (i < j) { int t = i; i = j;
 // below QP_REFINE_MERIT (late in the solve)
 #define QP_REFINE_ALPHA 0.5
 #define QP_REFINE_MERIT 1e6
-// relative threshold of the primal-infeasibility certificate (OSQP's eps_prim_inf analogue)
-#define QP_EPS_PINF 1e-6
+// relative threshold of the primal-infeasibility certificate: OSQP's default eps_prim_inf, the
+// value the reference's osqp.setup call runs with
+#define QP_EPS_PINF 1e-4
 
 // relative floor on D^-1 in the push-through blocks (K = D^-1 + G W^-1 G')
 template <typename T> constexpr double KFLOOR = sizeof(T) == 8 ? 1e-12 : 1e-6;
@@ -1813,11 +1815,11 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_update(const C
 // vmax receives (max -s, max -lambda) over this knot's rows.
 // Starting point after the initialization step: s = h - g'z at the new z for the present rows
 // (absent rows keep s = 1, lambda = 0: their affine step is zero).  Solo12: s and lambda floored
-// row by row at QP_INIT_FLOOR.  TALOS: vmax collects the largest violations for CVXOPT's shift of
-// every row (phase_init_shift).  On Solo12 the shift starts at mu ~ 700, far from the central
-// path (trot N=100: 9.3 Newton steps on average, 5.3 with the floors); on TALOS the floors were
-// not robust (oracle/ipm_mirror.py).  Branch-free with each row group's loads batched.
-#define QP_INIT_FLOOR 0.1
+// row by row (cmpc_qp_settings init_floor_s / _l, default 0.1).  TALOS, or floors 0: vmax
+// collects the largest violations for CVXOPT's shift of every row (phase_init_shift).  On Solo12
+// the shift starts at mu ~ 700, far from the central path (trot N=100 x 1024: 9.1 Newton steps
+// on average, max 12; 5.2, max 7 with the floors); on TALOS the floors were not robust
+// (oracle/ipm_mirror.py).  Branch-free with each row group's loads batched.
 template <typename T, int ROBOT>
 __device__ __forceinline__ void init_s_knot(const Ctx<T, ROBOT> &C, int k, T (&vmax)[2], const T *__restrict__ stp,
                                             const T *__restrict__ xs, const T *__restrict__ us,
@@ -1833,11 +1835,12 @@ __device__ __forceinline__ void init_s_knot(const Ctx<T, ROBOT> &C, int k, T (&v
     for (int i = 0; i < 3; ++i) x[i] = xs[(6 + i) * ld];
     for (int i = 0; i < NU; ++i) u[i] = us[i * ld];   // k = N: padding column (unused)
     const T t = ts[0];
+    const bool floors = ROBOT == 0 && C.fls > T(0);
     auto put = [&](int r, bool pr, T v) {   // v = g'z - h
         const T l = ls[r * ld];
-        if (ROBOT == 0) {
-            ss[r * ld] = pr ? fmax(-v, T(QP_INIT_FLOOR)) : T(1);
-            ls[r * ld] = pr ? fmax(l, T(QP_INIT_FLOOR)) : l;
+        if (floors) {
+            ss[r * ld] = pr ? fmax(-v, C.fls) : T(1);
+            ls[r * ld] = pr ? fmax(l, C.fll) : l;
         } else {
             ss[r * ld] = pr ? -v : T(1);
             vmax[0] = fmax(vmax[0], pr ? v : T(-1e300));
@@ -1917,7 +1920,7 @@ __device__ __forceinline__ T refine_direction(const Ctx<T, ROBOT> &C, T sigma_mu
 // ------------------------------------------------------------------ kernel
 template <typename T, int ROBOT>
 __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int only_active, int max_iter, T eps_abs, T eps_rel,
-                                               T eta) {
+                                               T eta, T floor_s, T floor_l) {
     extern __shared__ __attribute__((aligned(16))) unsigned char dsmem[];
     constexpr int NI = Rows<ROBOT>::NI;
     const int b = blockIdx.x;
@@ -1926,13 +1929,15 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
     __shared__ T red[8 * (NT / 64)];
     __shared__ T sh[2 * TW_SCRATCH];
     const int tid = threadIdx.x, N = d.N, K1 = N + 1, NB = N + 2, NBm = NB / 2;
-    Ctx<T, ROBOT> C{N, nullptr, nullptr, nullptr, nullptr, T(0), T(0), nullptr, nullptr, nullptr, nullptr, T(0), nullptr};
+    Ctx<T, ROBOT> C{N, nullptr, nullptr, nullptr, nullptr, T(0), T(0), nullptr, nullptr, nullptr, nullptr, T(0), T(0), T(0), nullptr};
     C.prm = d.params + d.class_id[b];
     C.stage = d.stage + (size_t)b * Stage<ROBOT>::SIZE * KPC;
     C.logic = d.logic + (size_t)b * N * Robot<ROBOT>::NC;
     C.xbar = d.Xbar + (size_t)b * K1 * 9;
     C.cw = d.cw[b];
     C.beta = C.prm->dt / C.prm->mass;
+    C.fls = floor_s;
+    C.fll = floor_l;
     {
         T wmax = T(1);
         for (int i = 0; i < 9; ++i) wmax = fmax(wmax, C.prm->Wx[i]);
@@ -2098,7 +2103,7 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
         if (init) {
             T vmax[2] = {T(-1e300), T(-1e300)};
             for (int k = tid; k < K1; k += NT) phase_init_step<T, ROBOT>(C, k, vmax);
-            if (ROBOT == 1) {   // CVXOPT shift (Solo12 floors inside init_s_knot)
+            if (ROBOT == 1 || !(C.fls > T(0))) {   // CVXOPT shift (Solo12 floors inside init_s_knot)
                 block_reduce<T, NT, 2, 1>(vmax, red);
                 const T sh_s = vmax[0] >= T(0) ? T(1) + vmax[0] : T(0);
                 const T sh_l = vmax[1] >= T(0) ? T(1) + vmax[1] : T(0);
@@ -2138,7 +2143,7 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
 #undef STAMP
 }
 
-#define INST(T, R) template __global__ void k_qp_ipm<T, R>(DevBuf<T>, int, int, T, T, T);
+#define INST(T, R) template __global__ void k_qp_ipm<T, R>(DevBuf<T>, int, int, T, T, T, T, T);
 INST(double, 0)
 INST(double, 1)
 INST(float, 0)

@@ -49,8 +49,10 @@ extern "C" {
  *   2  solved inaccurate: mu stalled for 3 iterations within 1e3 of the tolerance (the final
  *      merit is reported by cmpc_get_qp_info); a failure for the SCP loop, as in the reference
  *  -2  iteration cap
- *  -3  primal infeasible: Farkas certificate |E'nu + G'lambda| <= 1e-6 |(nu, lambda)|,
- *      b'nu + h'lambda <= -1e-6 |(nu, lambda)| on the diverging multipliers
+ *  -3  primal infeasible: Farkas certificate |E'nu + G'lambda| <= 1e-4 |(nu, lambda)|,
+ *      b'nu + h'lambda <= -1e-4 |(nu, lambda)| on the diverging multipliers (OSQP's default
+ *      eps_prim_inf); an infeasible QP whose multipliers have not diverged that far by the
+ *      iteration cap ends with -2
  *  -4  dual infeasible: never returned; P > 0 on (x, u) and the only other variable t has cost
  *      +1 with t >= 0, so the subproblem is bounded below
  * -10  non-finite values */
@@ -103,6 +105,10 @@ typedef struct {
     double eps_abs;         /* absolute tolerance (fp64 default 1e-10, fp32 1e-6) */
     double eps_rel;         /* relative tolerance (fp64 default 1e-10, fp32 1e-6) */
     double step_fraction;   /* fraction-to-boundary (default 0.99) */
+    /* Solo12 starting point: after the least-squares initialization step, s and lambda are
+     * floored row by row at these values (default 0.1, 0.1); 0 selects CVXOPT's shift of every
+     * row by 1 + the largest violation, which TALOS handles always use */
+    double init_floor_s, init_floor_l;
 } cmpc_qp_settings;
 
 /* Per-phase device timings of the last cmpc_scp_iterate (milliseconds, HIP events). */

@@ -79,11 +79,13 @@ def _fslot(qp):
     return 0 if qp.robot == 'solo12' else 2
 
 
-INIT_FLOOR = 0.1          # s, lambda floor of the Solo12 starting point
+INIT_FLOOR = 0.1          # s floor of the Solo12 starting point
+INIT_FLOOR_L = 0.1        # lambda floor
 
 
 def solve(qp, eps=1e-11, max_iter=60, eta=0.99, verbose=False, reg=0.0, piv_floor=1e-13, dcap_rel=1e12,
-          refine_alpha=0.5, refine_merit=1e6, eps_pinf=1e-6, init_floor=INIT_FLOOR):
+          refine_alpha=0.5, refine_merit=1e6, eps_pinf=1e-4, init_floor=INIT_FLOOR,
+          init_floor_l=INIT_FLOOR_L):
     N, nc, nu, nupc = qp.N, qp.nc, qp.nu, qp.nupc
     fo = _fslot(qp)
     talos = qp.robot != 'solo12'
@@ -162,7 +164,7 @@ def solve(qp, eps=1e-11, max_iter=60, eta=0.99, verbose=False, reg=0.0, piv_floo
     for it in range(0, max_iter + 1):
         # iteration 0 is the initialization step: one full Newton step from s = lambda = 1 (an
         # equality-constrained least-squares start).  Solo12: s and lambda are then floored row
-        # by row at INIT_FLOOR.  TALOS: CVXOPT's shift of every row by 1 + the largest violation.
+        # by row at INIT_FLOOR / INIT_FLOOR_L.  TALOS: CVXOPT's shift of every row by 1 + the largest violation.
         # On Solo12 the shift starts at mu ~ 700, far from the central path (trot N=100: 9.3
         # Newton steps on average, 5.3 with the floors); on TALOS the floors were not robust
         # (N=40: 22-24 steps against 18, one stall).
@@ -377,11 +379,11 @@ def solve(qp, eps=1e-11, max_iter=60, eta=0.99, verbose=False, reg=0.0, piv_floo
             vals = ineq_val(x, u, t)
             s_new = [-v * mk for v, mk in zip(vals, masks)]
             l_new = [(li + dli) * mk for li, dli, mk in zip(lam, dl, masks)]
-            if not talos:
+            if not talos and init_floor > 0:
                 # Solo12: per-row floors; rows the least-squares point violates start just inside
                 # the cone instead of every row shifting by the largest violation
                 s = [np.where(mk > 0, np.maximum(si, init_floor), 1.0) for si, mk in zip(s_new, masks)]
-                lam = [np.maximum(li, init_floor) * mk for li, mk in zip(l_new, masks)]
+                lam = [np.maximum(li, init_floor_l) * mk for li, mk in zip(l_new, masks)]
             else:
                 # TALOS: CVXOPT's shift by 1 + the largest violation
                 ap = max(float(-np.min(si[mk > 0])) for si, mk in zip(s_new, masks))
