@@ -28,6 +28,7 @@ template <typename T, int R> __global__ void k_default_controls(DevBuf<T>, T *);
 size_t ipm_lds_bytes(int N, int prec_bytes);
 template <typename T, int R> __global__ void k_accept(DevBuf<T>, int);
 template <typename T> __global__ void k_keep_accepted(DevBuf<T>);
+template <typename T> __global__ void k_knot_major(const T *, size_t, size_t, size_t, int, double *);
 template <typename T, int R> __global__ void k_rollout(DevBuf<T>, const T *, const T *, T *);
 size_t ipm_workspace_elems(int N, int robot);
 }  // namespace cmpc
@@ -231,20 +232,21 @@ void reset_scp(cmpc_handle h, const int32_t *class_id) {
 }
 
 // Knots [kn0, kn0 + n) of an element-major array (DevBuf::LS) into the knot-major host layout
-// dst[kn][e] (e < ne): one strided 2-D copy, transposed on the host.
+// dst[kn][e] (e < ne): transposed (and widened to fp64) on the device into the handle's scratch
+// buffer, then one contiguous copy.
 void dl_knots(cmpc_handle h, double *dst, const void *src, size_t kn0, size_t n, size_t ne) {
     if (!dst || n == 0) return;
-    const size_t es = h->esz(), LS = (size_t)h->max_batch * h->N;
-    std::vector<unsigned char> tmp(n * ne * es);
-    HIPCHK(hipMemcpy2DAsync(tmp.data(), n * es, (const char *)src + kn0 * es, LS * es, n * es, ne,
-                            hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
-    for (size_t e = 0; e < ne; ++e)
-        for (size_t k = 0; k < n; ++k) {
-            const size_t i = e * n + k;
-            dst[k * ne + e] = es == 8 ? reinterpret_cast<const double *>(tmp.data())[i]
-                                      : double(reinterpret_cast<const float *>(tmp.data())[i]);
-        }
+    const size_t LS = (size_t)h->max_batch * h->N;
+    double *tmp = (double *)h->scratch_bytes_at_least(n * ne * sizeof(double));
+    const dim3 grid((unsigned)((n + 31) / 32), (unsigned)((ne + 31) / 32));
+    if (h->prec == CMPC_PREC_F64)
+        hipLaunchKernelGGL((k_knot_major<double>), grid, dim3(256), 0, h->stream, (const double *)src, LS, kn0, n,
+                           (int)ne, tmp);
+    else
+        hipLaunchKernelGGL((k_knot_major<float>), grid, dim3(256), 0, h->stream, (const float *)src, LS, kn0, n,
+                           (int)ne, tmp);
+    HIPCHK(hipGetLastError());
+    from_dev_raw(h, dst, tmp, n * ne * sizeof(double));
 }
 
 std::vector<ScpState> get_scp(cmpc_handle h) {
@@ -344,6 +346,7 @@ int cmpc_destroy(cmpc_handle h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->comm && h->comm_free) h->comm_free(h->comm);
     for (void *p : h->allocs) (void)hipFree(p);
+    if (h->scratch) (void)hipFree(h->scratch);
     for (auto &e : h->ev)
         if (e) (void)hipEventDestroy(e);
     for (auto &a : h->ev_pool)

@@ -57,6 +57,9 @@ struct cmpc_handle_s {
     int comm_rank = 0, comm_size = 1;
     void (*comm_free)(void *) = nullptr;   // set by cmpc_comm_init, called by cmpc_destroy
     int plans_B = 0;   // problems whose contact plans were built on the device
+    // grow-only device scratch of the host getters (knot-major staging copies)
+    void *scratch = nullptr;
+    size_t scratch_bytes = 0;
 
     size_t esz() const { return prec == CMPC_PREC_F64 ? 8 : 4; }
     void *dalloc(size_t bytes) {
@@ -65,6 +68,19 @@ struct cmpc_handle_s {
         HIPCHK(hipMemsetAsync(p, 0, std::max<size_t>(bytes, 16), stream));
         allocs.push_back(p);
         return p;
+    }
+    void *scratch_bytes_at_least(size_t bytes) {
+        if (bytes > scratch_bytes) {
+            if (scratch) {
+                HIPCHK(hipStreamSynchronize(stream));
+                HIPCHK(hipFree(scratch));
+                scratch = nullptr;
+                scratch_bytes = 0;
+            }
+            HIPCHK(hipMalloc(&scratch, bytes));
+            scratch_bytes = bytes;
+        }
+        return scratch;
     }
     template <typename T> cmpc::DevBuf<T> buf() const {
         cmpc::DevBuf<T> d;

@@ -276,6 +276,28 @@ __global__ void __launch_bounds__(256) k_keep_accepted(DevBuf<T> d) {
     }
 }
 
+// Knots [kn0, kn0 + n) of an element-major array (element e of knot k at e * LS + k) into a
+// knot-major fp64 copy dst[k][e] for the host getters: 32 x 32 tiles through LDS, so both the
+// knot-contiguous reads and the element-contiguous writes are coalesced.
+template <typename T>
+__global__ void __launch_bounds__(256) k_knot_major(const T *src, size_t LS, size_t kn0, size_t n, int ne,
+                                                    double *dst) {
+    __shared__ double tile[32][33];
+    const size_t k0 = (size_t)blockIdx.x * 32;
+    const int e0 = blockIdx.y * 32, tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    for (int r = ty; r < 32; r += 8) {
+        const int e = e0 + r;
+        const size_t k = k0 + tx;
+        if (e < ne && k < n) tile[r][tx] = double(src[(size_t)e * LS + kn0 + k]);
+    }
+    __syncthreads();
+    for (int r = ty; r < 32; r += 8) {
+        const size_t k = k0 + r;
+        const int e = e0 + tx;
+        if (e < ne && k < n) dst[k * ne + e] = tile[tx][r];
+    }
+}
+
 // interpolate_SCP_solution (src/scp_solver.py:95-111) of the accepted solution, one thread per
 // (problem, output column, row): column i * ni + j = v_i + j * ((v_{i+1} - v_i) / ni).
 // X_out (B, 9, N * ni), U_out (B, nu, (N - 1) * ni), nu = nu_out (reference control width).
@@ -323,6 +345,8 @@ template __global__ void k_rollout<double, 1>(DevBuf<double>, const double *, co
 template __global__ void k_rollout<float, 0>(DevBuf<float>, const float *, const float *, float *);
 template __global__ void k_rollout<float, 1>(DevBuf<float>, const float *, const float *, float *);
 
+template __global__ void k_knot_major<double>(const double *, size_t, size_t, size_t, int, double *);
+template __global__ void k_knot_major<float>(const float *, size_t, size_t, size_t, int, double *);
 template __global__ void k_keep_accepted<double>(DevBuf<double>);
 template __global__ void k_keep_accepted<float>(DevBuf<float>);
 template __global__ void k_accept<double, 0>(DevBuf<double>, int);
