@@ -40,7 +40,7 @@ class Params(ctypes.Structure):
 class QPSettings(ctypes.Structure):
     _fields_ = [('max_iter', ctypes.c_int32), ('eps_abs', ctypes.c_double), ('eps_rel', ctypes.c_double),
                 ('step_fraction', ctypes.c_double), ('init_floor_s', ctypes.c_double),
-                ('init_floor_l', ctypes.c_double)]
+                ('init_floor_l', ctypes.c_double), ('waves_per_problem', ctypes.c_int32)]
 
 
 class Gait(ctypes.Structure):
@@ -212,7 +212,7 @@ class Solver:
 
     # ---- setup
     def set_qp_settings(self, max_iter=None, eps_abs=None, eps_rel=None, step_fraction=None, init_floor_s=None,
-                        init_floor_l=None):
+                        init_floor_l=None, waves_per_problem=None):
         s = QPSettings()
         self.lib.cmpc_default_qp_settings(self.prec, ctypes.byref(s))
         if max_iter is not None: s.max_iter = int(max_iter)
@@ -221,6 +221,7 @@ class Solver:
         if step_fraction is not None: s.step_fraction = float(step_fraction)
         if init_floor_s is not None: s.init_floor_s = float(init_floor_s)
         if init_floor_l is not None: s.init_floor_l = float(init_floor_l)
+        if waves_per_problem is not None: s.waves_per_problem = int(waves_per_problem)
         self._chk(self.lib.cmpc_set_qp_settings(self.h, ctypes.byref(s)), 'cmpc_set_qp_settings')
 
     def set_params(self, params):

@@ -21,11 +21,11 @@ template <typename T, int R> __global__ void k_linearize(DevBuf<T>, int);
 template <typename T, int R> __global__ void k_lin_knots(DevBuf<T>, int);
 template <typename T, int R> __global__ void k_cov_scan(DevBuf<T>, int);
 template <typename T, int R, bool FULL> __global__ void k_assemble(DevBuf<T>, int);
-template <typename T, int R> __global__ void k_qp_ipm(DevBuf<T>, int, int, T, T, T, T, T);
+template <typename T, int R, int NTT> __global__ void k_qp_ipm(DevBuf<T>, int, int, T, T, T, T, T);
 template <typename T> __global__ void k_interpolate(DevBuf<T>, int, int, T *, T *);
 template <typename T, int R> __global__ void k_contact_plan(DevBuf<T>, const cmpc_gait *, const T *, uint8_t *, T *, T *);
 template <typename T, int R> __global__ void k_default_controls(DevBuf<T>, T *);
-size_t ipm_lds_bytes(int N, int prec_bytes);
+size_t ipm_lds_bytes(int N, int prec_bytes, int nt);
 template <typename T, int R> __global__ void k_accept(DevBuf<T>, int);
 template <typename T> __global__ void k_keep_accepted(DevBuf<T>);
 template <typename T> __global__ void k_knot_major(const T *, size_t, size_t, size_t, int, double *);
@@ -95,6 +95,14 @@ template <typename T> DevParams<T> conv_params(const cmpc_params &p, int nw) {
     return d;
 }
 
+// QP waves per problem: the setting, or (0) two when the batch at two waves per problem still runs
+// in one round on the device (one wave per SIMD at ~500 registers per lane) and the horizon needs
+// more than one pass of 64 knots
+int qp_waves(cmpc_handle h) {
+    if (h->qs.waves_per_problem > 0) return h->qs.waves_per_problem;
+    return (h->N + 1 > 64 && 2L * h->B <= 4L * h->n_cu) ? 2 : 1;
+}
+
 template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int only_active) {
     DevBuf<T> d = h->buf<T>();
     const int B = h->B;
@@ -124,14 +132,21 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
         break;
     }
     case 2: {
-        // one workgroup per problem; three (N+2) x 9 block vectors in LDS (22 KB at N = 100 fp64),
-        // the Schur blocks in the workspace, so several problems share a CU
-        const size_t lds = ipm_lds_bytes(h->N, (int)sizeof(T));
-        HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_qp_ipm<T, R>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL((k_qp_ipm<T, R>), dim3(B), dim3(IPM_NT), lds, h->stream, d, only_active, h->qs.max_iter,
-                           T(h->qs.eps_abs), T(h->qs.eps_rel), T(h->qs.step_fraction), T(h->qs.init_floor_s),
-                           T(h->qs.init_floor_l));
+        // one workgroup per problem (one or two waves, cmpc_qp_settings::waves_per_problem); the
+        // (N+2) x 9 Schur vector and the sweep rings in LDS, the Schur blocks in the workspace
+        const int nt = 64 * qp_waves(h);
+        const size_t lds = ipm_lds_bytes(h->N, (int)sizeof(T), nt);
+        const void *fn = nt == 128 ? reinterpret_cast<const void *>(&k_qp_ipm<T, R, 128>)
+                                   : reinterpret_cast<const void *>(&k_qp_ipm<T, R, 64>);
+        HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        if (nt == 128)
+            hipLaunchKernelGGL((k_qp_ipm<T, R, 128>), dim3(B), dim3(128), lds, h->stream, d, only_active,
+                               h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), T(h->qs.step_fraction),
+                               T(h->qs.init_floor_s), T(h->qs.init_floor_l));
+        else
+            hipLaunchKernelGGL((k_qp_ipm<T, R, 64>), dim3(B), dim3(64), lds, h->stream, d, only_active,
+                               h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), T(h->qs.step_fraction),
+                               T(h->qs.init_floor_s), T(h->qs.init_floor_l));
         break;
     }
     case 3:
@@ -271,6 +286,7 @@ int cmpc_default_qp_settings(int precision, cmpc_qp_settings *s) {
     s->step_fraction = 0.99;
     s->init_floor_s = 0.1;
     s->init_floor_l = 0.1;
+    s->waves_per_problem = 0;
     return 0;
 }
 
@@ -292,6 +308,7 @@ int cmpc_create(cmpc_handle *out, int device, int robot, int N, int max_batch, i
         need(device >= 0 && device < ndev, "invalid device id");
         HIPCHK(hipSetDevice(device));
         HIPCHK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+        HIPCHK(hipDeviceGetAttribute(&h->n_cu, hipDeviceAttributeMultiprocessorCount, device));
         for (auto &e : h->ev) HIPCHK(hipEventCreate(&e));
         const size_t Bm = max_batch, K1 = N + 1, NB = N + 2, e = h->esz(), NC = h->NC;
         h->class_id = h->dalloc(Bm * 4);
@@ -359,7 +376,8 @@ int cmpc_destroy(cmpc_handle h) {
 int cmpc_set_qp_settings(cmpc_handle h, const cmpc_qp_settings *s) {
     return guard(h, [&] {
         need(s && s->max_iter > 0 && s->step_fraction > 0 && s->step_fraction < 1 && s->init_floor_s >= 0 &&
-                 s->init_floor_l >= 0 && (s->init_floor_s > 0) == (s->init_floor_l > 0), "invalid QP settings");
+                 s->init_floor_l >= 0 && (s->init_floor_s > 0) == (s->init_floor_l > 0) && s->waves_per_problem >= 0 &&
+                 s->waves_per_problem <= 2, "invalid QP settings");
         h->qs = *s;
     });
 }

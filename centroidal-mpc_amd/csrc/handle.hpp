@@ -29,6 +29,7 @@ struct Fail {
 struct cmpc_handle_s {
     int device = 0, robot = 0, N = 0, max_batch = 0, prec = 0, B = 0, n_classes = 0;
     int NC = 4, NI = 25, SS = 160;
+    int n_cu = 256;   // compute units of the device (QP waves-per-problem choice)
     hipStream_t stream = nullptr;
     hipEvent_t ev[5] = {};
     bool timed = false;

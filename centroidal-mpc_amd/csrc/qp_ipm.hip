@@ -34,7 +34,7 @@
 
 namespace cmpc {
 
-constexpr int NT = IPM_NT;   // one wave: a half-wave per end of the Schur sweeps; knots k, k + 64, ...
+// workgroup: NTT threads (template; 64 = one wave, 128 = two), knots k, k + NTT, ... per thread
 // Stored parts of the Phi factors (phase_factor -> phase_sblock); the w and direction phases
 // recompute everything they need (the trust-region Cholesky factor, each contact's G W^-1, Kinv,
 // F and W'^-1: tr_factor, fric_factor, fric_F, contact_wd), which costs less than its HBM round trip.
@@ -161,6 +161,9 @@ template <typename T, int ROBOT> struct Ctx {
     __device__ SV<T> bv(int f, int j) const { return SV<T>{ws + f * KPC + j}; }
     // contact-active bits of knot k, loaded once per phase (0 at k = N: only the TR rows exist)
     const LdsT<uint8_t> *cm = nullptr;   // per-knot contact masks in LDS (set once per solve)
+    // multi-wave workgroups: w_x of knot k (k >= 1) parked here by phase_w and added to Schur block
+    // k after the phase's barrier (add_wx), since block k's other terms come from another wave
+    LdsT<T> *wxs = nullptr;
     __device__ unsigned cmask(int k) const { return cm ? unsigned(cm[k]) : cmask_mem(k); }
     __device__ unsigned cmask_mem(int k) const {
         if (k >= N) return 0u;
@@ -1307,8 +1310,8 @@ __device__ void tw_solve_meet(const T *Ii, const T *Xs, int NB, int m, LdsT<T> *
 // The back sweep's local terms z_j = I_j y_j for every block but the meeting one, all blocks in
 // parallel (thread per block, in place in vb) once the elimination and the meeting block are
 // done: the sequential step is then a single 9-term product.
-template <typename T> __device__ void tw_solve_local(const T *Ii, int NB, int m, LdsT<T> *vb) {
-    for (int j = threadIdx.x; j < NB; j += NT) {
+template <typename T, int NTT> __device__ void tw_solve_local(const T *Ii, int NB, int m, LdsT<T> *vb) {
+    for (int j = threadIdx.x; j < NB; j += NTT) {
         if (j == m) continue;
         const T *I = Ii + (size_t)j * 81;   // packed
         T iv[45], y[9];
@@ -1483,10 +1486,19 @@ __device__ __forceinline__ void phase_w_core(const Ctx<T, ROBOT> &C, int k, int 
             opB<T, ROBOT>(st, ou, bu);
             for (int i = 0; i < 9; ++i) vb[(1 + k) * 9 + i] = r1[i] - (ax[i] + bu[i]);
         }
-        wave_sync();
-        if (k >= 1)
-            for (int i = 0; i < 9; ++i) vb[k * 9 + i] += wx[i];
+        if (C.wxs) {
+            if (k >= 1)
+                for (int i = 0; i < 9; ++i) C.wxs[k * 9 + i] = wx[i];
+        } else {
+            wave_sync();
+            if (k >= 1)
+                for (int i = 0; i < 9; ++i) vb[k * 9 + i] += wx[i];
+        }
     }
+}
+// the deferred last term of the fused right-hand side (multi-wave workgroups): block k += w_x,k
+template <typename T, int NTT> __device__ __forceinline__ void add_wx(LdsT<T> *vb, const LdsT<T> *wxs, int N) {
+    for (int e = 9 + (int)threadIdx.x; e < (N + 1) * 9; e += NTT) vb[e] += wxs[e];
 }
 template <typename T, int ROBOT> __device__ __forceinline__ void phase_w(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu) {
     using S = Stage<ROBOT>;
@@ -1893,40 +1905,44 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_init_shift(con
 // One step of iterative refinement of the corrector direction; returns the new step bound.
 // (Inlined: as an outlined call, the registers live across it were reloaded from scratch all over
 // the Newton step.)
-template <typename T, int ROBOT>
+template <typename T, int ROBOT, int NTT>
 __device__ __forceinline__ T refine_direction(const Ctx<T, ROBOT> &C, T sigma_mu, LdsT<T> *ring, LdsT<T> *shl,
                                                         T *red) {
     const int tid = threadIdx.x, K1 = C.N + 1, NB = C.N + 2, NBm = NB / 2;
-    for (int k = tid; k < K1; k += NT) phase_lres<T, ROBOT>(C, k, sigma_mu);
+    for (int k = tid; k < K1; k += NTT) phase_lres<T, ROBOT>(C, k, sigma_mu);
     __syncthreads();
-    for (int k = tid; k < K1; k += NT) phase_w<T, ROBOT>(C, k, 2, T(0));
+    for (int k = tid; k < K1; k += NTT) phase_w<T, ROBOT>(C, k, 2, T(0));
     __syncthreads();
-    tw_solve_elim<T>(C.So, NB, NBm, C.vb, ring);
+    if (NTT > 64) {
+        add_wx<T, NTT>(C.vb, C.wxs, C.N);
+        __syncthreads();
+    }
+    if (tid < 64) tw_solve_elim<T>(C.So, NB, NBm, C.vb, ring);
     __syncthreads();
     if (tid < 64) tw_solve_meet<T>(C.Sd, C.So, NB, NBm, C.vb, shl);
     __syncthreads();
-    tw_solve_local<T>(C.Sd, NB, NBm, C.vb);
+    tw_solve_local<T, NTT>(C.Sd, NB, NBm, C.vb);
     __syncthreads();
-    tw_solve_back<T>(C.So, NB, NBm, C.vb, ring);
+    if (tid < 64) tw_solve_back<T>(C.So, NB, NBm, C.vb, ring);
     __syncthreads();
     T ar[1] = {T(1)};
-    for (int k = tid; k < K1; k += NT) ar[0] = fmin(ar[0], phase_dz_refine<T, ROBOT>(C, k));
-    block_reduce<T, NT, 1, 2>(ar, red);   // (its barriers order the dnu reads before the sum)
-    for (int e = tid; e < NB * 9; e += NT) C.vb[e] += C.ws[(WF(dn0) + e % 9) * KPC + e / 9];
+    for (int k = tid; k < K1; k += NTT) ar[0] = fmin(ar[0], phase_dz_refine<T, ROBOT>(C, k));
+    block_reduce<T, NTT, 1, 2>(ar, red);   // (its barriers order the dnu reads before the sum)
+    for (int e = tid; e < NB * 9; e += NTT) C.vb[e] += C.ws[(WF(dn0) + e % 9) * KPC + e / 9];
     __syncthreads();
     return ar[0];
 }
 
 // ------------------------------------------------------------------ kernel
-template <typename T, int ROBOT>
-__global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int only_active, int max_iter, T eps_abs, T eps_rel,
+template <typename T, int ROBOT, int NTT>
+__global__ void __launch_bounds__(NTT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int only_active, int max_iter, T eps_abs, T eps_rel,
                                                T eta, T floor_s, T floor_l) {
     extern __shared__ __attribute__((aligned(16))) unsigned char dsmem[];
     constexpr int NI = Rows<ROBOT>::NI;
     const int b = blockIdx.x;
     if (b >= d.B) return;
     if (only_active && !d.scp[b].active) return;
-    __shared__ T red[8 * (NT / 64)];
+    __shared__ T red[8 * (NTT / 64)];
     __shared__ T sh[2 * TW_SCRATCH];
     const int tid = threadIdx.x, N = d.N, K1 = N + 1, NB = N + 2, NBm = NB / 2;
     Ctx<T, ROBOT> C{N, nullptr, nullptr, nullptr, nullptr, T(0), T(0), nullptr, nullptr, nullptr, nullptr, T(0), T(0), T(0), nullptr};
@@ -1951,13 +1967,14 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
     // contact masks of every knot, once per solve (each phase read them from global memory
     // first thing, and everything after waited on that load)
     __shared__ uint8_t cms[KPC];
-    for (int k = tid; k < K1; k += NT) cms[k] = (uint8_t)C.cmask_mem(k);
+    for (int k = tid; k < K1; k += NTT) cms[k] = (uint8_t)C.cmask_mem(k);
     C.cm = (const LdsT<uint8_t> *)cms;
     __syncthreads();
     // dynamic LDS: the (N+2) x 9 Schur vector, then two block rings per wave for the sweeps
     LdsT<T> *shl = (LdsT<T> *)sh;
     C.vb = (LdsT<T> *)reinterpret_cast<T *>(dsmem);
-    LdsT<T> *ring = C.vb + ((NB * 9 + 7) & ~7) + (tid >> 5) * SWEEP_LDS;   // per half-wave
+    LdsT<T> *ring = C.vb + ((NB * 9 + 7) & ~7) + ((tid & 63) >> 5) * SWEEP_LDS;   // per half-wave of wave 0
+    if (NTT > 64) C.wxs = C.vb + ((NB * 9 + 7) & ~7) + 2 * SWEEP_LDS;
     C.Sd = C.ws + Ws<ROBOT>::Sd;
     C.So = C.ws + Ws<ROBOT>::So;
 #ifdef CMPC_STAMPS
@@ -1972,7 +1989,7 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
 #define STAMP(i) do { } while (0)
 #endif
     // ---- starting point of the initialization step: z = (xlin, ulin, 0), nu = 0, s = lambda = 1
-    for (int k = tid; k < K1; k += NT) {
+    for (int k = tid; k < K1; k += NTT) {
         const SV<T> x = C.var_x(k);
         const T *xl = d.Xlin + ((size_t)b * K1 + k) * 9;   // start at the linearization point
         const T *ubar = d.Ulin + ((size_t)b * N + (k < N ? k : 0)) * NU;
@@ -1991,7 +2008,7 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
             dla[r] = T(0);
         }
     }
-    for (int j = tid; j < NB; j += NT) {
+    for (int j = tid; j < NB; j += NTT) {
         const SV<T> nu = C.bv(WF(nu), j);
         for (int i = 0; i < 9; ++i) nu[i] = T(0);
     }
@@ -2004,11 +2021,11 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
     for (it = 0; it <= max_iter; ++it) {
         const bool init = (it == 0);
         Norms<T, ROBOT> nm{0, 0, 0, 0, 0, 0, 0, 0};
-        for (int k = tid; k < K1; k += NT) phase_residual<T, ROBOT>(C, k, nm);
+        for (int k = tid; k < K1; k += NTT) phase_residual<T, ROBOT>(C, k, nm);
         T mx[6] = {nm.prim, nm.dual, nm.comp, nm.sp, nm.sd, nm.lmax};
-        block_reduce<T, NT, 6, 1>(mx, red);
+        block_reduce<T, NTT, 6, 1>(mx, red);
         T sm2[2] = {nm.mu, nm.cnt};
-        block_reduce<T, NT, 2, 0>(sm2, red);
+        block_reduce<T, NTT, 2, 0>(sm2, red);
         STAMP(0);
         const T prim = mx[0], dual = mx[1], comp = mx[2], sp = mx[3], sdd = mx[4];
         const T mu = sm2[0] / fmax(sm2[1], T(1));
@@ -2022,9 +2039,9 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
             // |E'nu + G'lambda| <= eps |(nu, lambda)| and b'nu + h'lambda <= -eps |(nu, lambda)|
             if (it >= 3 && prim > T(0.9) * prim_prev && merit > T(1e3)) {
                 T cm[2] = {T(0), mx[5]}, cs[1] = {T(0)};
-                for (int k = tid; k < K1; k += NT) phase_cert<T, ROBOT>(C, k, cm, cs[0]);
-                block_reduce<T, NT, 2, 1>(cm, red);
-                block_reduce<T, NT, 1, 0>(cs, red);
+                for (int k = tid; k < K1; k += NTT) phase_cert<T, ROBOT>(C, k, cm, cs[0]);
+                block_reduce<T, NTT, 2, 1>(cm, red);
+                block_reduce<T, NTT, 1, 0>(cs, red);
                 if (cm[0] <= T(QP_EPS_PINF) * cm[1] && cs[0] <= -T(QP_EPS_PINF) * cm[1]) {
                     status = CMPC_QP_PRIMAL_INFEASIBLE;
                     break;
@@ -2040,7 +2057,7 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
         if (it == max_iter) break;
         // ---- Phi factors and the predictor's particular solution (knot-local), then the S blocks
         // and the predictor's Schur right-hand side
-        for (int k = tid; k < K1; k += NT) {
+        for (int k = tid; k < K1; k += NTT) {
             KnotSL<T, ROBOT> kl;
             load_knot_sl(C, k, kl);
             phase_factor<T, ROBOT>(C, k, kl);
@@ -2048,15 +2065,18 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
         }
         __syncthreads();
         STAMP(1);
-        for (int k = tid; k < K1; k += NT) phase_sblock<T, ROBOT>(C, k);
+        if (NTT > 64) add_wx<T, NTT>(C.vb, C.wxs, N);
+        for (int k = tid; k < K1; k += NTT) phase_sblock<T, ROBOT>(C, k);
         __syncthreads();
         STAMP(2);
         // ---- factorization of S with the predictor's forward elimination fused in
+        if (tid < 64) {   // the recurrence runs on wave 0 (the other waves wait at the barrier)
 #ifdef CMPC_STAMPS
-        tw_factor_ends<T>(C.Sd, C.So, NB, NBm, shl, C.vb, d.stamps + (size_t)b * 16);
+            tw_factor_ends<T>(C.Sd, C.So, NB, NBm, shl, C.vb, d.stamps + (size_t)b * 16);
 #else
-        tw_factor_ends<T>(C.Sd, C.So, NB, NBm, shl, C.vb, nullptr);
+            tw_factor_ends<T>(C.Sd, C.So, NB, NBm, shl, C.vb, nullptr);
 #endif
+        }
         __syncthreads();
         if (tid < 64) tw_factor_meet<T>(C.Sd, C.So, NBm, shl, C.vb);
         __syncthreads();
@@ -2066,28 +2086,32 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
         T alpha = T(1);
         for (int corr = 0; corr < 2; ++corr) {
             if (corr) {
-                for (int k = tid; k < K1; k += NT) phase_w<T, ROBOT>(C, k, corr, sigma_mu);
+                for (int k = tid; k < K1; k += NTT) phase_w<T, ROBOT>(C, k, corr, sigma_mu);
                 __syncthreads();
+                if (NTT > 64) {
+                    add_wx<T, NTT>(C.vb, C.wxs, N);
+                    __syncthreads();
+                }
                 STAMP(4);
                 STAMP(5);   // (the right-hand side is formed inside phase_w)
-                tw_solve_elim<T>(C.So, NB, NBm, C.vb, ring);
+                if (tid < 64) tw_solve_elim<T>(C.So, NB, NBm, C.vb, ring);
                 __syncthreads();
                 if (tid < 64) tw_solve_meet<T>(C.Sd, C.So, NB, NBm, C.vb, shl);
                 __syncthreads();
             }
-            tw_solve_local<T>(C.Sd, NB, NBm, C.vb);
+            tw_solve_local<T, NTT>(C.Sd, NB, NBm, C.vb);
             __syncthreads();
-            tw_solve_back<T>(C.So, NB, NBm, C.vb, ring);
+            if (tid < 64) tw_solve_back<T>(C.So, NB, NBm, C.vb, ring);
             __syncthreads();
             STAMP(6);
             T am[1] = {T(1)}, mus[3] = {T(0), T(0), T(0)};
-            for (int k = tid; k < K1; k += NT) am[0] = fmin(am[0], phase_dz<T, ROBOT>(C, k, corr, init, mus));
-            block_reduce<T, NT, 1, 2>(am, red);
+            for (int k = tid; k < K1; k += NTT) am[0] = fmin(am[0], phase_dz<T, ROBOT>(C, k, corr, init, mus));
+            block_reduce<T, NTT, 1, 2>(am, red);
             STAMP(7);
             alpha = am[0];
             if (init) break;
             if (corr == 0) {   // Mehrotra centering from the affine step's complementarity
-                block_reduce<T, NT, 3, 0>(mus, red);
+                block_reduce<T, NTT, 3, 0>(mus, red);
                 const T mu_aff = (mus[0] + alpha * (mus[1] + alpha * mus[2])) / fmax(sm2[1], T(1));
                 const T sg = mu_aff / fmax(mu, T(1e-300));
                 sigma_mu = sg * sg * sg * mu;
@@ -2096,29 +2120,29 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
                 // one step of iterative refinement of the corrector direction (residual of the
                 // Newton system with the exact operators, correction solved with the same
                 // factorization; see oracle/ipm_mirror.py)
-                alpha = refine_direction<T, ROBOT>(C, sigma_mu, ring, shl, red);
+                alpha = refine_direction<T, ROBOT, NTT>(C, sigma_mu, ring, shl, red);
                 ++n_refine;
             }
         }
         if (init) {
             T vmax[2] = {T(-1e300), T(-1e300)};
-            for (int k = tid; k < K1; k += NT) phase_init_step<T, ROBOT>(C, k, vmax);
+            for (int k = tid; k < K1; k += NTT) phase_init_step<T, ROBOT>(C, k, vmax);
             if (ROBOT == 1 || !(C.fls > T(0))) {   // CVXOPT shift (Solo12 floors inside init_s_knot)
-                block_reduce<T, NT, 2, 1>(vmax, red);
+                block_reduce<T, NTT, 2, 1>(vmax, red);
                 const T sh_s = vmax[0] >= T(0) ? T(1) + vmax[0] : T(0);
                 const T sh_l = vmax[1] >= T(0) ? T(1) + vmax[1] : T(0);
-                for (int k = tid; k < K1; k += NT) phase_init_shift<T, ROBOT>(C, k, sh_s, sh_l);
+                for (int k = tid; k < K1; k += NTT) phase_init_shift<T, ROBOT>(C, k, sh_s, sh_l);
             }
             __syncthreads();
             continue;
         }
         alpha = fmin(T(1), eta * alpha);
-        for (int k = tid; k < K1; k += NT) phase_update<T, ROBOT>(C, k, alpha);
+        for (int k = tid; k < K1; k += NTT) phase_update<T, ROBOT>(C, k, alpha);
         __syncthreads();
         STAMP(8);
     }
     // ---- outputs: solution and multipliers
-    for (int k = tid; k < K1; k += NT) {
+    for (int k = tid; k < K1; k += NTT) {
         T x[9], u[NU], lm[NI];
         ldv(C.var_x(k), x);
         ldv(C.var_u(k), u);
@@ -2130,7 +2154,7 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
         for (int r = 0; r < NI; ++r)
             d.lams[((size_t)b * K1 + k) * NI + r] = Ctx<T, ROBOT>::present_m(msk, r) ? lm[r] : T(0);
     }
-    for (int e = tid; e < NB * 9; e += NT) d.nus[(size_t)b * NB * 9 + e] = C.ws[(WF(nu) + e % 9) * KPC + e / 9];
+    for (int e = tid; e < NB * 9; e += NTT) d.nus[(size_t)b * NB * 9 + e] = C.ws[(WF(nu) + e % 9) * KPC + e / 9];
     if (tid == 0) {
         d.qp_status[b] = status;
         d.qp_iters[b] = it;
@@ -2143,15 +2167,18 @@ __global__ void __launch_bounds__(NT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int on
 #undef STAMP
 }
 
-#define INST(T, R) template __global__ void k_qp_ipm<T, R>(DevBuf<T>, int, int, T, T, T, T, T);
+#define INST(T, R)                                                                       \
+    template __global__ void k_qp_ipm<T, R, 64>(DevBuf<T>, int, int, T, T, T, T, T);     \
+    template __global__ void k_qp_ipm<T, R, 128>(DevBuf<T>, int, int, T, T, T, T, T);
 INST(double, 0)
 INST(double, 1)
 INST(float, 0)
 INST(float, 1)
 #undef INST
 
-size_t ipm_lds_bytes(int N, int prec_bytes) {
-    return ((((size_t)(N + 2) * 9 + 7) & ~size_t(7)) + (size_t)2 * SWEEP_LDS) * prec_bytes;
+size_t ipm_lds_bytes(int N, int prec_bytes, int nt) {
+    const size_t vec = (((size_t)(N + 2) * 9 + 7) & ~size_t(7));
+    return (vec + (size_t)2 * SWEEP_LDS + (nt > 64 ? vec : 0)) * prec_bytes;   // + the w_x side array
 }
 
 size_t ipm_workspace_elems(int N, int robot) {

@@ -109,6 +109,10 @@ typedef struct {
      * floored row by row at these values (default 0.1, 0.1); 0 selects CVXOPT's shift of every
      * row by 1 + the largest violation, which TALOS handles always use */
     double init_floor_s, init_floor_l;
+    /* waves per problem of the QP workgroup: 1 (knots k, k + 64, ... on one wave) or 2 (the
+     * per-knot phases on two waves, the Schur recurrence on the first); 0 (default) picks 2 when
+     * two waves per problem still fit the device in one round (2 B <= 4 x CUs) and N + 1 > 64 */
+    int32_t waves_per_problem;
 } cmpc_qp_settings;
 
 /* Per-phase device timings of the last cmpc_scp_iterate (milliseconds, HIP events). */

@@ -1,0 +1,63 @@
+"""GPU: the QP kernel's one-wave and two-wave workgroups (cmpc_qp_settings.waves_per_problem)
+solve the same problems to the same answers.
+
+With two waves the per-knot phases run one knot per thread over 128 threads and the Schur
+recurrence stays on the first wave; the fused right-hand side's last term then crosses a wave
+boundary and goes through an LDS side array (qp_ipm.hip add_wx).  The two variants differ only
+in the summation order of the block-wide reductions.  On Solo12 problems statuses, Newton
+iteration counts and SCP decisions must agree and the solutions to 1e-9 relative.  TALOS QPs are
+ill-conditioned: a last-bit change in mu moves the Newton path (measured with
+scripts/waves_diag.py: +-1..2 Newton steps and 0.4-3.6e-6 relative solution differences at
+N = 100, 127 and 200, identically at one knot pass per thread, while each variant repeats
+bit-exactly), so there both must solve, iteration counts agree within 2 and solutions within the
+1e-5 parity bar of the oracle tests.  Horizons cover one knot pass (N = 63),
+exactly two waves (N = 127), the metric horizon, and TALOS at BASELINE C4's N = 200 (two passes
+of 128 knots); the last knot block straddles the wave boundary in all of them.
+"""
+import numpy as np
+import pytest
+
+from cmpc._lib import Solver
+from cmpc.synth import make_batch
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(pb, waves, steps=2):
+    s = Solver(pb.robot, pb.N, pb.B, 'fp64')
+    s.set_qp_settings(waves_per_problem=waves)
+    s.upload(pb)
+    out = []
+    for _ in range(steps):
+        s.scp_iterate(fixed_iters=True)
+        z, _, st, it = s.qp_solution(with_y=False)
+        out.append((z.copy(), st.copy(), it.copy(), s.iteration_log()['decision'].copy()))
+    s.close()
+    return out
+
+
+@pytest.mark.parametrize('cfg,N,B', [('trot', 63, 8), ('trot', 127, 8), ('trot', 100, 64), ('talos', 200, 16),
+                                     ('bound', 100, 8)])
+def test_two_wave_workgroup_matches_one_wave(cfg, N, B):
+    pb = make_batch(cfg, N, B, seed_offset=31)
+    one, two = _run(pb, 1), _run(pb, 2)
+    talos = cfg == 'talos'
+    for (z1, s1, i1, d1), (z2, s2, i2, d2) in zip(one, two):
+        assert np.all(s1 == 1) and np.all(s2 == 1), (s1, s2)
+        if talos:
+            assert np.abs(i1 - i2).max() <= 2, (i1, i2)
+        else:
+            np.testing.assert_array_equal(i1, i2)
+        np.testing.assert_array_equal(d1, d2)
+        err = np.abs(z1 - z2).max(axis=1) / np.abs(z1).max(axis=1)
+        assert err.max() <= (1e-5 if talos else 1e-9), err.max()
+
+
+def test_waves_setting_is_validated():
+    """waves_per_problem: 0 (auto, the default), 1 or 2; anything else is refused."""
+    pb = make_batch('trot', 20, 2)
+    s = Solver(pb.robot, 20, 2, 'fp64')
+    s.set_qp_settings(waves_per_problem=0)
+    with pytest.raises(Exception):
+        s.set_qp_settings(waves_per_problem=3)
+    s.close()

@@ -43,5 +43,5 @@ def test_default_qp_settings():
     lib = _lib.load()
     s = _lib.QPSettings()
     assert lib.cmpc_default_qp_settings(0, s) == 0
-    assert s.eps_abs == 1e-10 and s.eps_rel == 1e-10 and s.max_iter > 0
+    assert s.eps_abs == 1e-10 and s.eps_rel == 1e-10 and s.max_iter > 0 and s.waves_per_problem == 0
     assert lib.cmpc_default_qp_settings(1, s) == 0 and s.eps_abs == 1e-6
