@@ -155,7 +155,13 @@ def solve_scp(model, scp_params, gusto=False):
     """The reference's SCP loop for one model (reference :118-179), run on the device.
     ``gusto=True`` moves the linearization point to each accepted solution and iterates until
     convergence (the GuSTO scheme the reference cites, :113-117; include/cmpc.h
-    CMPC_SCP_MODE_GUSTO); the default reproduces the reference exactly (quirk Q1)."""
+    CMPC_SCP_MODE_GUSTO); the default reproduces the reference exactly (quirk Q1).
+
+    Returns the reference's dict of lists (state, control, gains, covs).  In reference mode the
+    loop ends at the first accepted iterate (Q1), so the lists hold exactly the reference's one
+    entry.  With ``gusto=True`` several iterates can be accepted; only the final one is returned
+    (the device keeps one accepted iterate per problem), where the reference's loop would append
+    each of them."""
     s = model._device_solver(None, scp_params)
     s.set_scp_mode('gusto' if gusto else 'reference')
     s.solve_scp(fixed_iters=False)
