@@ -66,7 +66,7 @@ EXPORTS = ['cmpc_create', 'cmpc_destroy', 'cmpc_last_error', 'cmpc_version', 'cm
            'cmpc_get_linearization_point', 'cmpc_interpolate', 'cmpc_generate_contact_plans',
            'cmpc_upload_states', 'cmpc_get_contact_plans', 'cmpc_get_warm_start', 'cmpc_get_qp_info',
            'cmpc_comm_get_unique_id', 'cmpc_comm_init', 'cmpc_comm_destroy', 'cmpc_comm_bcast_params',
-           'cmpc_comm_allreduce_max', 'cmpc_comm_gather_solution']
+           'cmpc_comm_allreduce_max', 'cmpc_comm_gather_solution', 'cmpc_load_qp']
 SCP_MODE = {'reference': 0, 'gusto': 1}
 
 _lib = None
@@ -128,6 +128,7 @@ def load():
         'cmpc_comm_bcast_params': (i32, [h, i32, i32, P(Params)]),
         'cmpc_comm_allreduce_max': (i32, [h, vp, i32]),
         'cmpc_comm_gather_solution': (i32, [h, i32, vp, vp, vp, vp, vp]),
+        'cmpc_load_qp': (i32, [h, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -342,6 +343,26 @@ class Solver:
         v = [np.zeros(1, np.int32) for _ in range(4)]
         self._chk(self.lib.cmpc_qp_sizes(self.h, *[_ptr(a) for a in v]), 'cmpc_qp_sizes')
         return tuple(int(a[0]) for a in v)
+
+    def load_qp(self, b, P, q, A, l, u):
+        """Problem b's QP from the reference's CSC layout (scipy sparse P, A; q, l, u) into the
+        device's structured form (cmpc_load_qp); raises CmpcError naming the offending row when the
+        QP lacks the stage structure."""
+        from scipy import sparse
+        P = sparse.csc_matrix(P); A = sparse.csc_matrix(A)
+        n, m = A.shape[1], A.shape[0]
+        if P.shape != (n, n):
+            raise CmpcError('P is %s, A has %d columns' % (P.shape, n))
+        big = 1e30
+        arrs = [np.ascontiguousarray(P.data, float), np.ascontiguousarray(P.indices, np.int32),
+                np.ascontiguousarray(P.indptr, np.int32), np.ascontiguousarray(q, float).ravel(),
+                np.ascontiguousarray(A.data, float), np.ascontiguousarray(A.indices, np.int32),
+                np.ascontiguousarray(A.indptr, np.int32),
+                np.ascontiguousarray(np.clip(np.asarray(l, float).ravel(), -big, big)),
+                np.ascontiguousarray(np.clip(np.asarray(u, float).ravel(), -big, big))]
+        if arrs[3].size != n or arrs[7].size != m or arrs[8].size != m:
+            raise CmpcError('q, l, u sizes do not match P, A')
+        self._chk(self.lib.cmpc_load_qp(self.h, int(b), n, m, *[_ptr(a) for a in arrs]), 'cmpc_load_qp')
 
     def export_qp(self, b):
         """(P, q, A, l, u) of problem b as scipy CSC, in the reference's row order."""

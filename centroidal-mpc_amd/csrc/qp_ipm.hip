@@ -251,6 +251,13 @@ __device__ __forceinline__ int p4(int i, int j) { if (i < j) { int t = i; i = j;
 
 // relative floor on D^-1 in the push-through blocks (K = D^-1 + G W^-1 G')
 template <typename T> constexpr double KFLOOR = sizeof(T) == 8 ? 1e-12 : 1e-6;
+// The friction block's floor is higher: at a zero contact force all four pyramid rows are active
+// and K tends to the rank-3 G W^-1 G' (four rows in 3-D), so a 1e-12 floor let cond(K) reach
+// 1e12, the direction's complementarity residual grew to 0.1-0.5 and refinement with the same
+// factor could not recover (TALOS QPs with other cost weights stalled at the iteration cap;
+// tests/test_gpu_load_qp.py, oracle/ipm_mirror.py).  At 1e-9 every such case solves, with fewer
+// refinements; only the direction is perturbed, the stopping test stays on the true residuals.
+template <typename T> constexpr double KFLOOR_FR = sizeof(T) == 8 ? 1e-9 : 1e-6;
 
 // in-place Cholesky of an 8x8 SPD matrix, packed lower (row j, col q <= j at j(j+1)/2 + q), with
 // a pivot floor relative to the original diagonal
@@ -324,7 +331,7 @@ __device__ __forceinline__ void fric_factor(const T (&G)[12], const T (&wi)[3], 
             Km[r][q] = acc;
         }
     for (int r = 0; r < 4; ++r) tr += Km[r][r];
-    const T kfloor = T(KFLOOR<T>) * tr + T(sizeof(T) == 8 ? 1e-300 : 1e-37);
+    const T kfloor = T(KFLOOR_FR<T>) * tr + T(sizeof(T) == 8 ? 1e-300 : 1e-37);
     for (int r = 0; r < 4; ++r) Km[r][r] += fmax(fdiv(s4[r], act ? l4[r] : T(1)), kfloor);
     inv4spd(Km, Ki);
     // masking by arithmetic (every value is finite: lambda -> 1 on inactive rows); per-lane

@@ -11,8 +11,10 @@ libcmpc.so on the GPU:
   device handle, one result per model.
 * ``sum_up_all_costs`` / ``stack_up_all_constraints`` / ``solve_subproblem`` keep the reference's
   step-by-step interface.  The QP they describe is the one assembled on the device, exported
-  in the reference's CSC layout; ``solve_subproblem`` solves it with the device QP solver
-  (structure-exploiting, so it accepts the QPs these two functions built, not arbitrary CSC).
+  in the reference's CSC layout; ``solve_subproblem`` solves it with the device QP solver.  A
+  QP built elsewhere (plain ``Cost`` / ``Constraint`` in the reference's layout) is decoded into
+  the device's structured form by ``cmpc_load_qp`` first; one without the stage structure is
+  refused with a ``CmpcError`` naming the offending row.
 
 The reference's OSQP call (eps 1e-7 + polish, src/scp_solver.py:59-68) is replaced by an
 interior-point method converged to 1e-11 (fp64): the QP's minimizer is unique (P > 0 on the
@@ -74,19 +76,49 @@ def convergence(traj_tuple_curr, traj_tuple_prev):
             np.linalg.norm(X_curr - X_prev, 2) / np.linalg.norm(X_curr, 2))
 
 
+_FOREIGN = {}
+
+
+def _foreign_solver(n, m):
+    """A one-problem device handle for a QP of n variables and m rows in the reference's layout:
+    n = 23 N + 10 for both robots; m = 38 N + 27 (Solo12) or 32 N + 27 (TALOS)."""
+    N = (n - 10) // 23
+    if N < 2 or 23 * N + 10 != n:
+        raise ValueError('%d variables is not the layout 9(N+1) + 12N + (N+1) + N of any horizon N' % n)
+    cfg = 'trot' if m == 38 * N + 27 else 'talos' if m == 32 * N + 27 else None
+    if cfg is None:
+        raise ValueError('%d rows is neither the Solo12 (%d) nor the TALOS (%d) layout at N = %d'
+                         % (m, 38 * N + 27, 32 * N + 27, N))
+    s = _FOREIGN.get((cfg, N))
+    if s is None:
+        from cmpc.synth import make_batch
+        pb = make_batch(cfg, N, 1)      # a valid problem to install the handle's sizes; load_qp replaces it
+        s = Solver(pb.robot, N, 1, 'fp64')
+        s.upload(pb)
+        _FOREIGN[(cfg, N)] = s
+    return s
+
+
 def solve_subproblem(cost, constraints):
-    """Solve the QP built by sum_up_all_costs / stack_up_all_constraints on the device;
-    returns (QP_FEASIBILITY, res) with res.x, res.y, res.info.status as OSQP's (reference :59-68)."""
+    """Solve the QP (cost.Q, cost.p, constraints.mat, constraints.lb, constraints.ub) on the device;
+    returns (QP_FEASIBILITY, res) with res.x, res.y, res.info.status as OSQP's (reference :59-68).
+
+    QPs built by sum_up_all_costs / stack_up_all_constraints are solved where the device assembled
+    them.  Any other QP in the reference's layout is decoded by cmpc_load_qp (csrc/load_qp.cpp: the
+    stage structure is checked row by row) into a one-problem handle of its robot and horizon."""
     model = getattr(constraints, '_model', None)
-    if model is None:
-        raise NotImplementedError('solve_subproblem solves the QPs assembled by stack_up_all_constraints (the '
-                                  'device solver exploits their stage structure); arbitrary CSC QPs are not '
-                                  'supported')
-    s, P, q, A, l, u = _device.export(model, constraints._traj, constraints._tr)
-    if getattr(cost, '_model', None) is not model:
-        if (cost.Q.shape != P.shape or abs(cost.Q - P).max() > 0 or
-                np.abs(np.asarray(cost.p) - q).max() > 1e-12 * max(1.0, np.abs(q).max())):
-            raise ValueError('the cost does not match the device assembly of this model')
+    same = model is not None and getattr(cost, '_model', None) is model
+    if model is not None and not same:
+        _, P, q, _, _, _ = _device.export(model, constraints._traj, constraints._tr)
+        same = (cost.Q.shape == P.shape and abs(cost.Q - P).max() == 0 and
+                np.abs(np.asarray(cost.p) - q).max() <= 1e-12 * max(1.0, np.abs(q).max()))
+    if same:
+        s, P, q, A, l, u = _device.export(model, constraints._traj, constraints._tr)
+    else:
+        P, q = cost.Q, np.asarray(cost.p, float)
+        A, l, u = constraints.mat, np.asarray(constraints.lb, float), np.asarray(constraints.ub, float)
+        s = _foreign_solver(A.shape[1], A.shape[0])
+        s.load_qp(0, P, q, A, l, u)
     s.qp_solve()
     z, y, st, it = s.qp_solution()
     x = z[0]

@@ -195,6 +195,17 @@ int cmpc_qp_sizes(cmpc_handle h, int32_t *n, int32_t *m, int32_t *nnzP, int32_t 
 int cmpc_export_qp(cmpc_handle h, int b, double *P_x, int32_t *P_i, int32_t *P_p, double *q, double *A_x,
                    int32_t *A_i, int32_t *A_p, double *l, double *u);
 /* z in the reference's variable layout (B, n) and y in its row layout (B, m). */
+/* Problem b's QP given in the reference's CSC layout (P, q, A, l, u as src/scp_solver.py:59-68
+ * hands them to OSQP; n variables, m rows, int32 indices) decoded into the device's structured
+ * form, for a following cmpc_qp_solve.  The QP must have the stage structure: the handle's sizes,
+ * a diagonal cost with one Wx / Wu for all knots, centroidal dynamics blocks, the reference's
+ * friction, CoP, trust-region and slack rows (csrc/load_qp.cpp lists every check).  Otherwise -2
+ * and a message naming the offending row.  Installs a parameter class with the decoded weights
+ * and dt / mass for problem b.  Replaces the OSQP call of solve_subproblem for QPs not built by
+ * cmpc_assemble. */
+int cmpc_load_qp(cmpc_handle h, int b, int n, int m, const double *P_x, const int32_t *P_i, const int32_t *P_p,
+                 const double *q, const double *A_x, const int32_t *A_i, const int32_t *A_p, const double *l,
+                 const double *u);
 int cmpc_get_qp_solution(cmpc_handle h, double *z, double *y, int32_t *status, int32_t *iters);
 /* Per-problem exit data of the last QP solve: final merit (<= 1 when solved) and the number of
  * iterative-refinement steps taken (B entries each; NULL skips). */

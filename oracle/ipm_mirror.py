@@ -85,7 +85,7 @@ INIT_FLOOR_L = 0.1        # lambda floor
 
 def solve(qp, eps=1e-11, max_iter=60, eta=0.99, verbose=False, reg=0.0, piv_floor=1e-13, dcap_rel=1e12,
           refine_alpha=0.5, refine_merit=1e6, eps_pinf=1e-4, init_floor=INIT_FLOOR,
-          init_floor_l=INIT_FLOOR_L):
+          init_floor_l=INIT_FLOOR_L, fric_floor=1e-9):
     N, nc, nu, nupc = qp.N, qp.nc, qp.nu, qp.nupc
     fo = _fslot(qp)
     talos = qp.robot != 'solo12'
@@ -257,8 +257,9 @@ def solve(qp, eps=1e-11, max_iter=60, eta=0.99, verbose=False, reg=0.0, piv_floo
         Gw = np.einsum('kirm,kimn->kirn', qp.G, Winv[:, :, fo:fo + 3, fo:fo + 3])    # G W^-1 (N,nc,4,3)
         Dinv_f = np.where(fm > 0, s[2] / np.where(fm > 0, lam[2], 1.0), 1.0)
         GWG = np.einsum('kirn,kiqn->kirq', Gw, qp.G)
-        # floor on D^-1: at a zero force all four pyramid rows are active (degenerate, K -> rank 3)
-        kfloor = 1e-12 * np.trace(GWG, axis1=2, axis2=3)[..., None] + 1e-300
+        # floor on D^-1: at a zero force all four pyramid rows are active (degenerate, K -> rank 3);
+        # kernel KFLOOR_FR (1e-9; 1e-12 before round 2's TALOS weight cases)
+        kfloor = fric_floor * np.trace(GWG, axis1=2, axis2=3)[..., None] + 1e-300
         Kf = GWG + np.maximum(Dinv_f, kfloor)[..., None] * np.eye(4)
         Kf = np.where(fm[..., None] > 0, Kf, np.eye(4))                 # inactive contacts: identity
         Gw = Gw * fm[..., None]

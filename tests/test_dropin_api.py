@@ -68,9 +68,9 @@ def test_interpolation_and_solution_reshape_match_oracle():
     assert S.convergence(dict(state=X, control=U), dict(state=X, control=U)) == 0.0
 
 
-def test_foreign_qp_is_rejected_and_missing_warm_start_raises(tmp_path, monkeypatch):
+def test_qp_of_no_layout_is_rejected_and_missing_warm_start_raises(tmp_path, monkeypatch):
     from scipy import sparse
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(ValueError, match='variables'):   # before any device call
         S.solve_subproblem(Cost(Q=sparse.eye(3), p=np.zeros(3)), Constraint(mat=sparse.eye(3), lb=-np.ones(3),
                                                                             ub=np.ones(3)))
     import types
@@ -82,3 +82,14 @@ def test_foreign_qp_is_rejected_and_missing_warm_start_raises(tmp_path, monkeypa
     monkeypatch.chdir(tmp_path)     # no wholeBody_to_centroidal_traj.npz here
     with pytest.raises(FileNotFoundError):
         Centroidal_model(conf)
+
+
+def test_foreign_qp_layout_inference_rejects_other_sizes():
+    """solve_subproblem on a QP not built by the drop-in infers robot and horizon from the
+    reference's layout (n = 23 N + 10; m = 38 N + 27 Solo12, 32 N + 27 TALOS) before any device
+    call, and refuses sizes of no layout."""
+    from src.scp_solver import _foreign_solver
+    with pytest.raises(ValueError, match='variables'):
+        _foreign_solver(23 * 30 + 11, 38 * 30 + 27)
+    with pytest.raises(ValueError, match='rows'):
+        _foreign_solver(23 * 30 + 10, 38 * 30 + 28)

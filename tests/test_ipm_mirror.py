@@ -40,12 +40,15 @@ def _struct(cfg, N, b, weight, radius, edit=None):
 
 
 def test_talos_problem_280_needs_refinement():
+    """Round 1's C4 stall (friction floor 1e-12, as then): it stalls without refinement and solves
+    with it; the round-2 friction floor (1e-9) solves it as well."""
     N = 200
     qp, ref_qp = _struct('talos', N, 280, 500.0, 100.0)
-    plain = IM.solve(qp, refine_alpha=0.0)
+    plain = IM.solve(qp, refine_alpha=0.0, fric_floor=1e-12)
     assert plain['status'] == 2 and plain['merit'] > 1.0          # the stall, reproduced on the CPU
-    sol = IM.solve(qp)
+    sol = IM.solve(qp, fric_floor=1e-12)
     assert sol['status'] == 1 and sol['merit'] <= 1.0 and sol['n_refine'] >= 1
+    assert IM.solve(qp)['status'] == 1
     ref = sparse_ipm_qp(*ref_qp)
     assert ref.info.status == 'solved'
     nx = 9 * (N + 1)
@@ -73,3 +76,35 @@ def test_primal_infeasible_certificate():
     # Newton step, so detection takes ~40 steps at N=30; the iteration cap is 60)
     assert sol['status'] == -3 and sol['iters'] <= 50
     assert admm_qp(*ref_qp).info.status == 'primal infeasible'
+
+
+def test_talos_zero_force_friction_floor():
+    """TALOS with other cost weights (state weights x (2, 2, 0.5, 1, 1, 1, 3, 3, 3), control weights
+    x 0.25): contact forces reach the pyramid's apex, where all four friction rows are active and
+    K = D^-1 + G W^-1 G' tends to rank 3.  At the old 1e-12 floor the direction's complementarity
+    residual stays at 0.1-0.5 and the solve hits the iteration cap; at the kernel's 1e-9 it solves
+    and matches the sparse IPM on the same QP."""
+    N = 40
+    pb = make_batch('talos', N, 1, seed_offset=0)
+    p = pb.oracle_problem(0)
+    par = pb.params[0]
+    td = M.compute_trajectory_data(p['Xbar'], p['Ubar'], p['logic'], p['pos'], p['rot'], p['prm'])
+    sp = p['scp_params']
+    wx = np.asarray(par.Wx) * np.array([2.0, 2.0, 0.5, 1.0, 1.0, 1.0, 3.0, 3.0, 3.0])
+    wu = np.asarray(par.Wu) * 0.25
+    qp = IM.StructQP.from_arrays(N, par.robot, pb.nc, wx, wu, pb.Xbar[0], pb.Ubar[0], td['f_x'], td['f_u'],
+                                 td['dynamics'].T, pb.logic[0], pb.rot[0], par.mu, sp['omega0'],
+                                 sp['trust_region_radius0'], tracking=par.tracking, foot_range=par.foot_range)
+    assert IM.solve(qp, fric_floor=1e-12)['status'] == -2
+    sol = IM.solve(qp)
+    assert sol['status'] == 1 and sol['merit'] <= 1.0
+    prm = dict(p['prm'])
+    prm['Wx'] = np.diag(wx); prm['Wu'] = np.diag(wu)
+    P, q = T.build_cost(N, prm, p['Xbar'])
+    A, l, u = T.build_constraints(N, prm, p['logic'], p['pos'], p['rot'], p['Xbar'], p['Ubar'], td, sp['omega0'],
+                                  sp['trust_region_radius0'])
+    ref = sparse_ipm_qp(P, q, A, l, u)
+    assert ref.info.status == 'solved'
+    nx = 9 * (N + 1)
+    z = IM.to_z(qp, sol)
+    assert np.abs(z[:nx] - ref.x[:nx]).max() <= 1e-6 * np.abs(ref.x[:nx]).max()
