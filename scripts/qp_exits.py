@@ -1,6 +1,7 @@
 """Diagnostic: QP exit statuses, final merits and refinement counts of K fixed-K SCP iterations of a
 synthetic batch.  Usage: python scripts/qp_exits.py <cfg> <N> <B> <iters> [fp64|fp32] [eps ...]
-(several eps values: one run per value, each timed: QP ms from HIP events)"""
+(several eps values: one run per value, each timed: QP ms from HIP events; a value written
+eta=<v> sets the step fraction instead of eps)"""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, 'centroidal-mpc_amd')]
@@ -9,12 +10,14 @@ from cmpc._lib import Solver
 from cmpc.synth import make_batch
 cfg, N, B, K = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
 prec = sys.argv[5] if len(sys.argv) > 5 else 'fp64'
-epss = [float(v) for v in sys.argv[6:]] or [None]
+epss = sys.argv[6:] or [None]
 pb = make_batch(cfg, N, B) if cfg != 'mixed' else make_batch('trot', N, B, mixed=('pace', 'trot'))
 s = Solver(pb.robot, N, B, prec)
 for eps in epss:
-  if eps is not None:
-    s.set_qp_settings(eps_abs=eps, eps_rel=eps)
+  if eps is not None and eps.startswith('eta='):
+    s.set_qp_settings(step_fraction=float(eps[4:]))
+  elif eps is not None:
+    s.set_qp_settings(eps_abs=float(eps), eps_rel=float(eps))
   s.upload(pb)
   print('eps', eps)
   for k in range(K):
