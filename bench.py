@@ -11,9 +11,10 @@ here by ``--gpus N`` (cmpc/shard.py spawn_local; the parent never touches the GP
 only over RCCL through libcmpc's C ABI (no PyTorch): rank 0 broadcasts the parameter classes, an
 RCCL max-reduction is the barrier around the timed region and takes the max time over ranks, and
 the accepted solutions are gathered to rank 0 after it (timed separately: ``gather_ms``).
-``value`` is weak scaling (1024 problems per GPU, no data-path collective: the path shards into
-independent problems); ``strong_scaling`` times the same steps with the global batch fixed at
-1024 split over the GPUs.
+``value`` is strong scaling, as BASELINE.json's metric reads ("batch=1024 @ 1/2/4/8 GPU"): the
+global batch (``--batch``, 1024) split into contiguous slices over the GPUs (no
+data-path collective: the path shards into independent problems).  At N > 1 ``weak_scaling``
+times the same steps with 1024 problems on every GPU.  ``--scaling weak`` swaps the two.
 
 Extra fields ("Measurement"):
   roofline      QP kernel: algorithmic bytes per launch (SURVEY.md 8d per-IPM-iteration figure,
@@ -178,13 +179,14 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=2)
-    ap.add_argument('--batch', type=int, default=1024, help='problems per GPU (weak scaling)')
-    ap.add_argument('--global-batch', type=int, default=1024, help='strong-scaling global batch')
+    ap.add_argument('--batch', type=int, default=1024,
+                    help='global batch (strong scaling, the metric) or problems per GPU (--scaling weak)')
+    ap.add_argument('--scaling', choices=('strong', 'weak'), default='strong')
     ap.add_argument('--N', type=int, default=100)
     ap.add_argument('--config', default='trot')
     ap.add_argument('--precision', default='fp64')
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--no-extras', action='store_true', help='skip strong-scaling and early-exit legs')
+    ap.add_argument('--no-extras', action='store_true', help='skip the other-scaling and early-exit legs')
     args = ap.parse_args()
 
     from cmpc.shard import RcclComm, shard_bounds, spawn_local, world_from_env
@@ -195,8 +197,18 @@ def main():
 
     from cmpc._lib import Solver
 
-    pb = make_problems(args.config, args.N, args.batch, rank * args.batch)
-    solver = Solver(pb.robot, args.N, args.batch, args.precision, device=local_rank)
+    def slice_of(mode):
+        """(first global problem, problems on this rank, problems per step over all ranks)"""
+        if mode == 'strong':
+            if args.batch < world:
+                raise SystemExit('global batch %d < %d ranks' % (args.batch, world))
+            lo, hi = shard_bounds(args.batch, rank, world)
+            return lo, hi - lo, args.batch
+        return rank * args.batch, args.batch, args.batch * world
+
+    lo, nb, units_step = slice_of(args.scaling)
+    pb = make_problems(args.config, args.N, nb, lo)
+    solver = Solver(pb.robot, args.N, nb, args.precision, device=local_rank)
     comm = RcclComm(solver, rank, world, addr, port) if world > 1 else None
     if comm is not None:
         comm.bcast_params(pb.params if rank == 0 else None, capacity=len(pb.params))
@@ -210,13 +222,12 @@ def main():
     _, _, qst, _ = solver.qp_solution(with_y=False)
     merit, nref = solver.qp_info()
     gather_ms = None
-    if comm is not None:
+    if comm is not None and units_step == nb * world:   # the RCCL gather sends equal slices
         comm.barrier()
         tg = time.perf_counter()
         comm.gather_solution(root=0)
         gather_ms = float(comm.allreduce_max([time.perf_counter() - tg])[0]) * 1e3
-    units = args.batch * world * args.steps
-    value = units / elapsed
+    value = units_step * args.steps / elapsed
     w = 8 if args.precision in ('fp64', 'f64', 'float64') else 4
     n_steps = max(tim['iterations'], 1)
     qp_mean_s = tim['qp_ms'] / 1e3 / n_steps
@@ -224,7 +235,7 @@ def main():
     compulsory = compulsory_qp_bytes(args.N, ipm_total, w, pb.robot) / qp_mean_s / 1e9
     traffic = None
     pmc = os.path.join(ROOT, 'profiles', 'qp_pmc_traffic.json')
-    metric_config = (args.config, args.N, args.batch, w) == ('trot', 100, 1024, 8)
+    metric_config = (args.config, args.N, nb, w) == ('trot', 100, 1024, 8)
     if metric_config and os.path.exists(pmc):   # the PMC summary was measured on the metric config only
         try:
             traffic = json.load(open(pmc)).get('hbm_bytes_per_launch')
@@ -240,16 +251,16 @@ def main():
         'warmup': args.warmup,
         'ms_per_step': elapsed / args.steps * 1e3,
         'higher_is_better': True,
-        'scaling': 'weak',
+        'scaling': args.scaling,
         'vs_baseline': None,
         'dtype': 'f64' if w == 8 else 'f32',
         'data': 'synthetic (seeded contact plans + dynamically consistent warm starts, cmpc/synth.py)',
-        'config': {'workload': '%s SCP iterations (fixed-K), N=%d, %d problems per GPU'
-                               % (WORKLOAD_NAMES.get(args.config, args.config), args.N, args.batch),
-                   'config': args.config, 'N': args.N, 'batch_per_gpu': args.batch,
-                   'global_batch': args.batch * world, 'parallelism': 'batch-sharded x%d (RCCL)' % world},
+        'config': {'workload': '%s SCP iterations (fixed-K), N=%d, %d problems over %d GPU(s) (%d on rank 0)'
+                               % (WORKLOAD_NAMES.get(args.config, args.config), args.N, units_step, world, nb),
+                   'config': args.config, 'N': args.N, 'batch_per_gpu': nb,
+                   'global_batch': units_step, 'parallelism': 'batch-sharded x%d (RCCL)' % world},
         'phase_ms_per_step': {k: tim[k] / n_steps for k in ('linearize_ms', 'assemble_ms', 'qp_ms', 'accept_ms')},
-        'qp_ipm_iterations_mean': ipm_total / args.batch,
+        'qp_ipm_iterations_mean': ipm_total / nb,
         'qp_exit': {'status_counts': {str(int(a)): int(b) for a, b in zip(u, c)},
                     'merit_max': float(merit.max()), 'refined_problems': int((nref > 0).sum()),
                     'refine_steps': int(nref.sum())},
@@ -260,20 +271,20 @@ def main():
     if gather_ms is not None:
         out['gather_ms'] = gather_ms
     if not args.no_extras:
-        # strong scaling: the global batch fixed, contiguous slices over the ranks
+        # the other scaling mode at N > 1: weak (1024 problems on every GPU) beside the strong
+        # headline, or strong (the global batch split) beside a weak one
         if world > 1:
-            lo, hi = shard_bounds(args.global_batch, rank, world)
-            per = -(-args.global_batch // world)
-            pbs = make_problems(args.config, args.N, per, lo)
-            s2 = Solver(pbs.robot, args.N, per, args.precision, device=local_rank)
+            other = 'weak' if args.scaling == 'strong' else 'strong'
+            lo2, nb2, units2 = slice_of(other)
+            pbs = make_problems(args.config, args.N, nb2, lo2)
+            s2 = Solver(pbs.robot, args.N, nb2, args.precision, device=local_rank)
             s2.upload(pbs)
             for _ in range(args.warmup):
                 s2.scp_iterate(fixed_iters=True)
             el2, _ = timed_steps(s2, comm, args.steps)
             s2.close()
-            out['strong_scaling'] = {'global_batch': args.global_batch, 'per_gpu': per,
-                                     'value': args.global_batch * args.steps / el2,
-                                     'ms_per_step': el2 / args.steps * 1e3}
+            out[other + '_scaling'] = {'global_batch': units2, 'per_gpu': nb2,
+                                       'value': units2 * args.steps / el2, 'ms_per_step': el2 / args.steps * 1e3}
         # early exit, the reference's loop semantics, device-resident inputs, outputs copied back
         solver.upload(pb, set_params=comm is None)
         solver.synchronize()
