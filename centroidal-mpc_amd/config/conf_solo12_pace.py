@@ -47,6 +47,12 @@ beta_u = 0.01
 state_cost_weights = np.diag([1e4, 1e4, 1e4, 1e3, 1e3, 1e3, 1e5, 1e5, 1e5])
 control_cost_weights = np.diag([1e2, 1e2, 1e1] * 4)
 
+# whole-body task weights (conf_solo12_pace.py:90-92): read by the whole-body stage only (out of scope),
+# kept so scripts that read the attribute run unchanged
+whole_body_task_weights = {'footTrack': {'swing': 1e5, 'impact': 1e6}, 'impulseVel': 20, 'comTrack': 1000, 'stateBounds': 0e3,
+                           'stateReg': {'stance': 0.1, 'impact': 1}, 'ctrlReg': {'stance': 1, 'impact': 10}, 'frictionCone': 2,
+                           'centroidalTrack': 1e4, 'contactForceTrack': 100}
+
 # SCP solver parameters (conf_solo12_pace.py:96-98)
 scp_params = {'trust_region_radius0': 50, 'omega0': 100, 'omega_max': 1e10, 'epsilon': 1e-6, 'rho0': 0.4,
               'rho1': 1.5, 'beta_succ': 2., 'beta_fail': 0.5, 'gamma_fail': 5, 'convergence_threshold': 1e-3,
@@ -57,3 +63,4 @@ WITH_MESHCAT_DISPLAY = False
 WITH_PYBULLET_SIMULATION = False
 WITHPLOT = False
 SAVEDAT = False
+cameraTF = [2., 2.68, 0.84, 0.2, 0.62, 0.72, 0.22]  # viewer camera (conf_solo12_pace.py:101)

@@ -23,6 +23,12 @@ gait_templates, contact_sequence = create_contact_sequence(dt, gait, ee_frame_na
 N = plan_length(contact_sequence, dt)
 N_ctrl = int((N - 1) * (dt / dt_ctrl))
 
+# whole-body task weights (conf_talos.py:26-28): read by the whole-body stage only (out of scope),
+# kept so scripts that read the attribute run unchanged
+whole_body_task_weights = {'footTrack': {'swing': 1e8, 'impact': 1e8}, 'impulseVel': 1e6, 'comTrack': 1e6, 'stateBounds': 0e3,
+                           'stateReg': {'stance': 1e1, 'impact': 1e1}, 'ctrlReg': {'stance': 1e-3, 'impact': 1e-3}, 'frictionCone': 10,
+                           'centroidalTrack': 1e4, 'contactForceTrack': 100}
+
 # ---- synthetic centroidal parameters (absent from the reference config) ----
 robot_name = 'TALOS'
 gravity_constant = -9.81
@@ -46,3 +52,4 @@ scp_params = {'trust_region_radius0': 100, 'omega0': 100, 'omega_max': 1e10, 'ep
               'rho1': 1.5, 'beta_succ': 2., 'beta_fail': 0.5, 'gamma_fail': 5, 'convergence_threshold': 1e-3,
               'max_iterations': 10}
 WITHDISPLAY = False
+cameraTF = [3., 3.68, 0.84, 0.2, 0.62, 0.72, 0.22]  # viewer camera (conf_talos.py:42)
