@@ -68,6 +68,10 @@ template <typename T> __device__ __forceinline__ T rcp_nr(T p) {
 }
 // LDS-qualified element type (keeps ds_* instructions in outlined helpers)
 template <typename T> using LdsT = __attribute__((address_space(3))) T;
+// global-qualified element type: in an outlined helper a plain T * is a flat pointer, and flat
+// loads count in both vmcnt and lgkmcnt, so every LDS wait would also wait for the HBM loads in
+// flight (the meeting block's operands, the sweep's next chunk of blocks)
+template <typename T> using GlbT = __attribute__((address_space(1))) T;
 
 // a / b as a * (1 / b): the IEEE fp64 division is a ~10-instruction sequence; the reciprocal with
 // two Newton steps is within an ulp or two, which the interior-point iteration does not notice
@@ -875,7 +879,7 @@ constexpr int TW_SCRATCH = 5 * 88 + 16;
 //   Oq, Iq: Y = Oq Iq, A -= Y Oq'   (meeting block only)
 template <typename T, int L>
 __device__ __forceinline__ void tw_step(const LdsT<T> *Dn, const LdsT<T> *Op, const LdsT<T> *Ip, const LdsT<T> *Oq,
-                                        const LdsT<T> *Iq, T *Xout, T *Yout, T *Iout, LdsT<T> *A, LdsT<T> *P,
+                                        const LdsT<T> *Iq, GlbT<T> *Xout, GlbT<T> *Yout, GlbT<T> *Iout, LdsT<T> *A, LdsT<T> *P,
                                         LdsT<T> *Xb, LdsT<T> *Dd, LdsT<T> *vb = nullptr, int j = 0, int jx = 0,
                                         int jy = 0, unsigned long long *sub = nullptr) {
     constexpr int NE = (81 + L - 1) / L;
@@ -1007,7 +1011,7 @@ __device__ __forceinline__ void tw_step(const LdsT<T> *Dn, const LdsT<T> *Op, co
 // the stored upper triangle U.  The inverse is mirrored into P (full, for the next step) and
 // stored packed into Iout.
 template <typename T>
-__device__ __forceinline__ void tw_step_sym(const LdsT<T> *Dn, const LdsT<T> *Op, const LdsT<T> *Ip, T *Xout, T *Iout,
+__device__ __forceinline__ void tw_step_sym(const LdsT<T> *Dn, const LdsT<T> *Op, const LdsT<T> *Ip, GlbT<T> *Xout, GlbT<T> *Iout,
                                             LdsT<T> *A, LdsT<T> *P, LdsT<T> *Xb, LdsT<T> *Dd, LdsT<T> *vb, int j,
                                             int jx, unsigned long long *sub = nullptr) {
 #ifdef CMPC_STAMPS
@@ -1128,7 +1132,8 @@ __device__ __forceinline__ void tw_step_sym(const LdsT<T> *Dn, const LdsT<T> *Op
 // the compiler drain the whole memory queue (this step's stores included) at the loop header.
 // The bottom end lands its coupling block S_{j,j+1} transposed, so both ends run the same step.
 template <typename T>
-__device__ void tw_factor_ends(T *Sd, T *So, int NB, int m, LdsT<T> *sh, LdsT<T> *vb, unsigned long long *stamp_out) {
+__device__ void tw_factor_ends(T *Sd_, T *So_, int NB, int m, LdsT<T> *sh, LdsT<T> *vb, unsigned long long *stamp_out) {
+    GlbT<T> *Sd = (GlbT<T> *)Sd_, *So = (GlbT<T> *)So_;
     constexpr int NE = 3;
     const int lane = threadIdx.x & 63, l = lane & 31;
     const bool top = lane < 32;
@@ -1151,7 +1156,7 @@ __device__ void tw_factor_ends(T *Sd, T *So, int NB, int m, LdsT<T> *sh, LdsT<T>
     unsigned long long sub[4] = {0, 0, 0, 0};
     unsigned long long *subp = (stamp_out && top) ? sub : nullptr;
     {
-        const T *D0 = Sd + (size_t)j0 * 81;
+        const GlbT<T> *D0 = Sd + (size_t)j0 * 81;
         T v[NE];
 #pragma unroll
         for (int q = 0; q < NE; ++q) v[q] = D0[ep[q]];
@@ -1163,7 +1168,7 @@ __device__ void tw_factor_ends(T *Sd, T *So, int NB, int m, LdsT<T> *sh, LdsT<T>
         const bool act = s < nstep;
         // raw blocks of the next step (clamped past the end: branch-free loads)
         const int jn = s + 1 < nstep ? j + dj : j;
-        const T *On = So + (size_t)(top ? (jn > 0 ? jn - 1 : 0) : jn) * 81, *Dnx = Sd + (size_t)jn * 81;
+        const GlbT<T> *On = So + (size_t)(top ? (jn > 0 ? jn - 1 : 0) : jn) * 81, *Dnx = Sd + (size_t)jn * 81;
         T pv[NE], nv[NE];
 #pragma unroll
         for (int q = 0; q < NE; ++q) { pv[q] = On[ec[q]] * em[q]; nv[q] = Dnx[ep[q]]; }
@@ -1189,13 +1194,14 @@ __device__ void tw_factor_ends(T *Sd, T *So, int NB, int m, LdsT<T> *sh, LdsT<T>
 }
 
 // the meeting block (whole wave): I_{m-1} and I_{m+1} are the two halves' previous inverses in LDS
-template <typename T> __device__ void tw_factor_meet(T *Sd, T *So, int m, LdsT<T> *sh, LdsT<T> *vb) {
+template <typename T> __device__ void tw_factor_meet(T *Sd_, T *So_, int m, LdsT<T> *sh, LdsT<T> *vb) {
+    GlbT<T> *Sd = (GlbT<T> *)Sd_, *So = (GlbT<T> *)So_;
     const int lane = threadIdx.x & 63;
     const int e0 = lane, e1 = lane + 64;
     const bool has1 = e1 < 81;
     LdsT<T> *A = sh, *P = A + 88, *Xb = A + 176, *Op = A + 264, *Dd = A + 352;
     LdsT<T> *Pq = sh + TW_SCRATCH + 88, *Oq = sh + TW_SCRATCH + 264;
-    auto cpl = [&](const T *blk, int e) -> T {   // compact coupling block -> element e (zero off-pattern)
+    auto cpl = [&](const GlbT<T> *blk, int e) -> T {   // compact coupling block -> element e (zero off-pattern)
         const int c = cp9(e / 9, e % 9);
         return blk[c >= 0 ? c : 0] * (c >= 0 ? T(1) : T(0));
     };
@@ -1219,7 +1225,7 @@ template <typename T> __device__ void tw_factor_meet(T *Sd, T *So, int m, LdsT<T
 // index past the end re-reads the last block).
 constexpr int RSLOT = 88;
 template <typename T, int K, bool PK = false> struct ChunkStream {   // PK: packed symmetric blocks
-    const T *base;   // block i at base + i * step
+    const GlbT<T> *base;   // block i at base + i * step
     long step;
     int n;
     LdsT<T> *buf;    // 2 x K slots of RSLOT
@@ -1229,7 +1235,7 @@ template <typename T, int K, bool PK = false> struct ChunkStream {   // PK: pack
 #pragma unroll
         for (int q = 0; q < K; ++q) {
             const int i = c * K + q;
-            const T *p = base + (i < n ? i : n - 1) * step;
+            const GlbT<T> *p = base + (i < n ? i : n - 1) * step;
 #pragma unroll
             for (int g = 0; g < 3; ++g) {
                 const int el = l + 32 * g < 81 ? l + 32 * g : 80;
@@ -1265,7 +1271,8 @@ template <typename T> __device__ void tw_solve_elim(const T *Xs, int NB, int m, 
     const int lr = l < 9 ? l : 0;
     // step i: top j = i + 1 (X_j at So[i]); bottom j = NB - 2 - i (Y_j at So[NB - 2 - i])
     const int n = top ? m - 1 : NB - 2 - m, nmax = m - 1;
-    ChunkStream<T, KE> X{top ? Xs : Xs + (size_t)(NB - 2) * 81, top ? 81L : -81L, n > 0 ? n : 1, ring, {}};
+    const GlbT<T> *Xg = (const GlbT<T> *)Xs;
+    ChunkStream<T, KE> X{top ? Xg : Xg + (size_t)(NB - 2) * 81, top ? 81L : -81L, n > 0 ? n : 1, ring, {}};
     X.issue(0);
     X.land(0);
     for (int c = 0; c * KE < nmax; ++c) {
@@ -1300,14 +1307,14 @@ __device__ void tw_solve_meet(const T *Ii, const T *Xs, int NB, int m, LdsT<T> *
     const int lane = threadIdx.x & 63;
     if (lane < 9) {
         T v = vb[m * 9 + lane];
-        const T *X = Xs + (size_t)(m - 1) * 81 + lane * 9, *Y = Xs + (size_t)m * 81 + lane * 9;
+        const GlbT<T> *X = (const GlbT<T> *)Xs + (size_t)(m - 1) * 81 + lane * 9, *Y = (const GlbT<T> *)Xs + (size_t)m * 81 + lane * 9;
         const LdsT<T> *yp = vb + (m - 1) * 9, *yn = vb + (m + 1) * 9;
         for (int q = 0; q < 9; ++q) v = fma(-X[q], yp[q], fma(-Y[q], yn[q], v));
         sh[lane] = v;
     }
     wave_sync();
     if (lane < 9) {
-        const T *I = Ii + (size_t)m * 81;   // packed
+        const GlbT<T> *I = (const GlbT<T> *)Ii + (size_t)m * 81;   // packed
         T v = T(0);
         for (int q = 0; q < 9; ++q) v = fma(I[pk9(lane, q)], sh[q], v);
         vb[m * 9 + lane] = v;
@@ -1320,7 +1327,7 @@ __device__ void tw_solve_meet(const T *Ii, const T *Xs, int NB, int m, LdsT<T> *
 template <typename T, int NTT> __device__ void tw_solve_local(const T *Ii, int NB, int m, LdsT<T> *vb) {
     for (int j = threadIdx.x; j < NB; j += NTT) {
         if (j == m) continue;
-        const T *I = Ii + (size_t)j * 81;   // packed
+        const GlbT<T> *I = (const GlbT<T> *)Ii + (size_t)j * 81;   // packed
         T iv[45], y[9];
 #pragma unroll
         for (int p = 0; p < 45; ++p) iv[p] = I[p];
@@ -1343,7 +1350,7 @@ __device__ void tw_solve_back(const T *Xs, int NB, int m, LdsT<T> *vb, LdsT<T> *
     // step i: top j = m - 1 - i (X_{j+1} at So[j]); bottom j = m + 1 + i (Y_{j-1} at So[j-1]);
     // vb[j] holds z_j = I_j y_j (tw_solve_local)
     const int n = top ? m : NB - 1 - m, nmax = m;
-    ChunkStream<T, KE> X{Xs + (size_t)(top ? m - 1 : m) * 81, top ? -81L : 81L, n > 0 ? n : 1, ring, {}};
+    ChunkStream<T, KE> X{(const GlbT<T> *)Xs + (size_t)(top ? m - 1 : m) * 81, top ? -81L : 81L, n > 0 ? n : 1, ring, {}};
     X.issue(0);
     X.land(0);
     for (int c = 0; c * KE < nmax; ++c) {
