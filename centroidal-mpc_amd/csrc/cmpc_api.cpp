@@ -152,7 +152,8 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
     case 3:
         hipLaunchKernelGGL((k_accept<T, R>), dim3(B), dim3(64), 0, h->stream, d, only_active ? 0 : 1);   // ACC_NT
         {
-            const int per = (h->N + 1) * 90 + h->N * NU * 10;   // X, Sigma | U, K elements per problem
+            const int per = h->ks_live ? (h->N + 1) * 9 + h->N * NU                // X | U
+                                       : (h->N + 1) * 90 + h->N * NU * 10;   // X, Sigma | U, K elements per problem
             hipLaunchKernelGGL((k_keep_accepted<T>), dim3((unsigned)std::min(16, (per + 255) / 256), B), dim3(256), 0,
                                h->stream, d);
         }
@@ -235,6 +236,7 @@ void phase(cmpc_handle h, int ph, int only_active) {
 }
 
 void reset_scp(cmpc_handle h, const int32_t *class_id) {
+    h->ks_live = h->scp_mode == CMPC_SCP_MODE_REFERENCE;
     std::vector<ScpState> st(h->B);
     for (int b = 0; b < h->B; ++b) {
         const cmpc_params &p = h->hparams[class_id[b]];
@@ -262,6 +264,21 @@ void dl_knots(cmpc_handle h, double *dst, const void *src, size_t kn0, size_t n,
                            (int)ne, tmp);
     HIPCHK(hipGetLastError());
     from_dev_raw(h, dst, tmp, n * ne * sizeof(double));
+}
+
+// Reference mode serves accepted K / Sigma from the live arrays (cmpc_handle_::ks_live); before
+// anything can make them differ from the accepted iteration's (GuSTO mode moves the linearization
+// point, new contact plans change it), they are copied to Kacc / Sacc once and copied per accept
+// from then on.
+void materialize_accepted_ks(cmpc_handle h) {
+    if (!h->ks_live) return;
+    if (h->B > 0) {
+        const size_t e = h->esz();
+        HIPCHK(hipMemcpyAsync(h->Kacc, h->K, (size_t)h->max_batch * h->N * NU * 9 * e, hipMemcpyDeviceToDevice, h->stream));
+        HIPCHK(hipMemcpyAsync(h->Sacc, h->Sig, (size_t)h->max_batch * (h->N + 1) * 81 * e, hipMemcpyDeviceToDevice, h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+    }
+    h->ks_live = false;
 }
 
 std::vector<ScpState> get_scp(cmpc_handle h) {
@@ -469,6 +486,7 @@ int cmpc_set_trust_region(cmpc_handle h, const double *weight, const double *rad
 
 int cmpc_generate_contact_plans(cmpc_handle h, int B, const cmpc_gait *gaits, const double *foot0) {
     return guard(h, [&] {
+        materialize_accepted_ks(h);   // the accepted K / Sigma belong to the old plans
         need(B >= 1 && B <= h->max_batch, "batch size out of range");
         need(gaits && foot0, "null input buffer");
         for (int b = 0; b < B; ++b) {
@@ -544,6 +562,7 @@ int cmpc_get_warm_start(cmpc_handle h, double *Xbar, double *Ubar) {
 int cmpc_set_scp_mode(cmpc_handle h, int mode) {
     return guard(h, [&] {
         need(mode == CMPC_SCP_MODE_REFERENCE || mode == CMPC_SCP_MODE_GUSTO, "unknown SCP mode");
+        if (mode != CMPC_SCP_MODE_REFERENCE) materialize_accepted_ks(h);
         h->scp_mode = mode;
     });
 }
@@ -838,8 +857,8 @@ int cmpc_get_solution(cmpc_handle h, double *X, double *U, double *K, double *Si
         };
         dl(X, h->Xacc, B * K1 * 9);
         dl(U, h->Uacc, B * N * NU);
-        dl_knots(h, K, h->Kacc, 0, B * N, NU * 9);
-        dl(Sigma, h->Sacc, B * K1 * 81);
+        dl_knots(h, K, h->ks_live ? h->K : h->Kacc, 0, B * N, NU * 9);
+        dl(Sigma, h->ks_live ? h->Sig : h->Sacc, B * K1 * 81);
         auto st = get_scp(h);
         for (size_t b = 0; b < B; ++b) {
             if (n_accepted) n_accepted[b] = st[b].n_accepted;

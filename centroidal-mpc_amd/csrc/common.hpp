@@ -70,6 +70,7 @@ template <typename T> struct DevBuf {
     const T *Xbar, *Ubar;    // (B,N+1,9) (B,N,NU) warm start: tracking reference, boundary states
     T *Xlin, *Ulin;          // (B,N+1,9) (B,N,NU) linearization point (= warm start in reference mode)
     int scp_mode;            // CMPC_SCP_MODE_*
+    int copy_ks;             // k_keep_accepted also copies K, Sigma (see cmpc_handle_::ks_live)
     // linearization.  The per-knot arrays are element-major: element e of knot kn = b * N + k at
     // X[e * LS + kn] (LS = max_batch * N), so the knot-per-lane kernels read and write them
     // coalesced; the C ABI getters transpose to the knot-major layouts of include/cmpc.h.

@@ -51,6 +51,13 @@ struct cmpc_handle_s {
          *Xacc = nullptr, *Uacc = nullptr, *Kacc = nullptr, *Sacc = nullptr, *stamps = nullptr, *Xlin = nullptr,
          *Ulin = nullptr;
     int scp_mode = CMPC_SCP_MODE_REFERENCE;
+    // Reference mode never moves the linearization point (quirk Q1), so every SCP iteration
+    // recomputes bit-identical K and Sigma from the same inputs: an accepted iteration's gains and
+    // covariances are the live arrays, and k_keep_accepted copies only X and U (the reference
+    // keeps references to that iteration's arrays, no copy).  Cleared (after copying the live
+    // arrays into Kacc / Sacc) when the mode turns to GuSTO or the contact plans change; set
+    // again by the next upload.
+    bool ks_live = true;
     bool lin_lane = true;   // knot-per-lane linearization (diagonal R); else k_linearize
     bool lin_lane_done = false;   // the last linearization came from k_lin_knots (stage partly written)
     // RCCL communicator of the batch split (comm.cpp); nullptr until cmpc_comm_init
@@ -89,7 +96,7 @@ struct cmpc_handle_s {
         d.class_id = (const int32_t *)class_id; d.params = (const cmpc::DevParams<T> *)params;
         d.logic = (const uint8_t *)logic; d.pos = (const T *)pos; d.rot = (const T *)rot;
         d.Xbar = (const T *)Xbar; d.Ubar = (const T *)Ubar;
-        d.Xlin = (T *)Xlin; d.Ulin = (T *)Ulin; d.scp_mode = scp_mode;
+        d.Xlin = (T *)Xlin; d.Ulin = (T *)Ulin; d.scp_mode = scp_mode; d.copy_ks = ks_live ? 0 : 1;
         d.f = (T *)f; d.A = (T *)A; d.Bu = (T *)Bu; d.C = (T *)C; d.K = (T *)K; d.Sig = (T *)Sig;
         d.Acl = (T *)Acl; d.Qw = (T *)Qw; d.stage = (T *)stage; d.cw = (T *)cw;
         d.LS = (size_t)max_batch * N;

@@ -245,10 +245,11 @@ __global__ void __launch_bounds__(ACC_NT) k_accept(DevBuf<T> d, int fixed_iters)
     }
 }
 
-// Accepted iterations keep X, U and this iteration's LQR gains / covariances (and, GuSTO mode,
-// become the linearization point): a grid over (element chunk, problem), so the ~170 KB per
+// Accepted iterations keep X, U and (d.copy_ks) this iteration's LQR gains / covariances (and, GuSTO
+// mode, become the linearization point): a grid over (element chunk, problem), so the ~170 KB per
 // accepted problem stream at HBM rate (one wave per problem copying them latency-bound took
-// ~200 us per SCP iteration at batch 1024, N = 100).
+// ~200 us per SCP iteration at batch 1024, N = 100).  In reference mode the gains and covariances
+// are served from the live arrays (cmpc_handle_::ks_live) and only X, U are copied.
 template <typename T>
 __global__ void __launch_bounds__(256) k_keep_accepted(DevBuf<T> d) {
     const int b = blockIdx.y;
@@ -257,7 +258,8 @@ __global__ void __launch_bounds__(256) k_keep_accepted(DevBuf<T> d) {
     const int nx = K1 * 9, nu = N * NU, nk = N * NU * 9, ns = K1 * 81;
     const bool gusto = d.scp_mode == CMPC_SCP_MODE_GUSTO;
     const T *Xs = d.xs + (size_t)b * nx, *Us = d.us + (size_t)b * nu;
-    for (int e = blockIdx.x * 256 + threadIdx.x; e < nx + nu + nk + ns; e += gridDim.x * 256) {
+    const int ne = nx + nu + (d.copy_ks ? nk + ns : 0);
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < ne; e += gridDim.x * 256) {
         if (e < nx) {
             d.Xacc[(size_t)b * nx + e] = Xs[e];
             if (gusto) d.Xlin[(size_t)b * nx + e] = Xs[e];

@@ -80,3 +80,31 @@ def test_device_interpolation_matches_reference_formula():
                 Xr[:, i * ni + j] = X[:, i] + j * dx
         np.testing.assert_allclose(Xi[b], Xr, rtol=1e-14, atol=1e-14)
         np.testing.assert_allclose(Ui[b], Ur, rtol=1e-14, atol=1e-14)
+
+
+def test_accepted_gains_and_covariances_survive_mode_switch():
+    """Reference mode serves an accepted iteration's K and Sigma from the live linearization
+    arrays (the linearization point never moves, quirk Q1, so they are that iteration's arrays,
+    as the reference keeps references to them); switching to GuSTO mode first copies them, so
+    the accepted results are bit-identical before and after the switch and after a GuSTO-mode
+    iteration that moves the linearization point."""
+    pb = make_batch('trot', 30, 3)
+    with Solver(pb.robot, 30, 3, 'fp64') as s:
+        s.upload(pb)
+        s.solve_scp(fixed_iters=False)
+        sol = s.solution()
+        assert np.all(sol['n_accepted'] >= 1)
+        lin = s.linearization()
+        np.testing.assert_array_equal(sol['K'], lin['K'])
+        np.testing.assert_array_equal(sol['Sigma'], lin['Sigma'])
+        s.set_scp_mode('gusto')
+        sol2 = s.solution()
+        np.testing.assert_array_equal(sol2['K'], sol['K'])
+        np.testing.assert_array_equal(sol2['Sigma'], sol['Sigma'])
+        s.linearize()          # the same inputs: the live arrays are recomputed, the accepted copies stay
+        s.set_trust_region(radius=np.full(3, 1e-9))   # every further iteration rejects: nothing new accepted
+        s.scp_iterate(fixed_iters=True)
+        sol3 = s.solution()
+        np.testing.assert_array_equal(sol3['n_accepted'], sol['n_accepted'])
+        np.testing.assert_array_equal(sol3['K'], sol['K'])
+        np.testing.assert_array_equal(sol3['Sigma'], sol['Sigma'])
