@@ -18,7 +18,7 @@
 
 namespace cmpc {
 template <typename T, int R> __global__ void k_linearize(DevBuf<T>, int);
-template <typename T, int R> __global__ void k_lin_knots(DevBuf<T>, int);
+template <typename T, int R> __global__ void k_lin_knots(DevBuf<T>, int, int);
 template <typename T, int R> __global__ void k_cov_scan(DevBuf<T>, int);
 template <typename T, int R, bool FULL> __global__ void k_assemble(DevBuf<T>, int);
 template <typename T, int R, int NTT> __global__ void k_qp_ipm(DevBuf<T>, int, int, T, T, T, T, T);
@@ -111,12 +111,18 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
     case 0:
         // one knot per lane (diagonal R; also writes the linearization part of the stage records),
         // or one workgroup per problem (general R); then the per-problem covariance scan
+        // Reference mode skips the dense A, Bu, C (nothing in the SCP loop reads them: the QP uses
+        // the stage record, k_accept the closed form); GuSTO mode keeps them, since its
+        // linearization point moves and the getters could not recompute them later.
         if (h->lin_lane) {
             const long n = (long)B * h->N;
+            const int dense = h->scp_mode == CMPC_SCP_MODE_GUSTO ? 1 : 0;
             hipLaunchKernelGGL((k_lin_knots<T, R>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream, d,
-                               only_active);
+                               only_active, dense);
+            h->lin_dense = dense != 0;
         } else {
             hipLaunchKernelGGL((k_linearize<T, R>), dim3(B), dim3(256), 0, h->stream, d, only_active);
+            h->lin_dense = true;
         }
         h->lin_lane_done = h->lin_lane;
         hipLaunchKernelGGL((k_cov_scan<T, R>), dim3(B), dim3(64), 0, h->stream, d, only_active);
@@ -225,6 +231,25 @@ template <typename T, int R> void rollout_impl(cmpc_handle h, const double *X, c
     from_dev<T>(h, out, dO, nx);
 }
 
+// The dense A, Bu, C for the getters and the CSC export: reference mode's SCP loop does not store
+// them (launch_phase, case 0); its linearization point never moves (quirk Q1), so one more
+// k_lin_knots pass over every problem rewrites the same values and adds the dense arrays.
+template <typename T, int R> void ensure_dense_impl(cmpc_handle h) {
+    DevBuf<T> d = h->buf<T>();
+    const long n = (long)h->B * h->N;
+    hipLaunchKernelGGL((k_lin_knots<T, R>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream, d, 0, 1);
+    HIPCHK(hipGetLastError());
+}
+void ensure_dense(cmpc_handle h) {
+    if (h->lin_dense || !h->lin_lane_done || h->B == 0) return;
+    if (h->prec == CMPC_PREC_F64) {
+        if (h->robot == 0) ensure_dense_impl<double, 0>(h); else ensure_dense_impl<double, 1>(h);
+    } else {
+        if (h->robot == 0) ensure_dense_impl<float, 0>(h); else ensure_dense_impl<float, 1>(h);
+    }
+    h->lin_dense = true;
+}
+
 void phase(cmpc_handle h, int ph, int only_active) {
     need(h->B > 0, "no problems uploaded");
     need(h->n_classes > 0, "parameters not set");
@@ -237,6 +262,7 @@ void phase(cmpc_handle h, int ph, int only_active) {
 
 void reset_scp(cmpc_handle h, const int32_t *class_id) {
     h->ks_live = h->scp_mode == CMPC_SCP_MODE_REFERENCE;
+    h->lin_lane_done = false;   // new inputs: nothing to recompute densely until the next linearization
     std::vector<ScpState> st(h->B);
     for (int b = 0; b < h->B; ++b) {
         const cmpc_params &p = h->hparams[class_id[b]];
@@ -659,6 +685,7 @@ int cmpc_synchronize(cmpc_handle h) { return guard(h, [&] { HIPCHK(hipStreamSync
 int cmpc_get_linearization(cmpc_handle h, double *f, double *A, double *Bu, double *C, double *K, double *Sigma) {
     return guard(h, [&] {
         const size_t B = h->B, N = h->N, NC = h->NC;
+        ensure_dense(h);
         auto dl = [&](double *dst, void *src, size_t n) {
             if (h->prec == CMPC_PREC_F64) from_dev<double>(h, dst, src, n); else from_dev<float>(h, dst, src, n);
         };
@@ -688,6 +715,7 @@ int cmpc_export_qp(cmpc_handle h, int b, double *P_x, int32_t *P_i, int32_t *P_p
     return guard(h, [&] {
         need(b >= 0 && b < h->B, "problem index out of range");
         const int N = h->N, NC = h->NC, K1 = N + 1, NUPC = NU / NC, FO = h->robot == 0 ? 0 : 2, SS = h->SS;
+        ensure_dense(h);
         const int n = 9 * K1 + NU * N + K1 + N;
         auto dl = [&](std::vector<double> &dst, void *src, size_t off, size_t cnt) {
             dst.resize(cnt);

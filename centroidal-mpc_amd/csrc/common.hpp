@@ -169,4 +169,37 @@ template <typename A, typename B, typename T> __device__ __forceinline__ void cr
     o[2] = a[0] * b[1] - a[1] * b[0];
 }
 
+// (shared by k_lin_knots, which writes the dense B, and k_accept's linear prediction)
+// rows 3..8 of the per-contact input matrix B_c (6 x NUPC) of contact c
+template <typename T, int ROBOT> struct ContactB {
+    static constexpr int NUPC = Robot<ROBOT>::NUPC;
+    T b[6][NUPC];
+};
+
+template <typename T, int ROBOT>
+__device__ __forceinline__ void contact_B(T dta, const T (&lev)[3], const T *f, const T *Rc, ContactB<T, ROBOT> &B) {
+    constexpr int NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
+    const T sk[3][3] = {{T(0), -lev[2], lev[1]}, {lev[2], T(0), -lev[0]}, {-lev[1], lev[0], T(0)}};
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+        for (int q = 0; q < NUPC; ++q) B.b[a][q] = T(0);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        B.b[q][FO + q] = dta;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) B.b[3 + r][FO + q] = dta * sk[r][q];
+    }
+    if (ROBOT == 1) {
+        const T fs[3][3] = {{T(0), -f[2], f[1]}, {f[2], T(0), -f[0]}, {-f[1], f[0], T(0)}};
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+#pragma unroll
+            for (int q = 0; q < 2; ++q)   // d/dcop [(R2 cop) x f] = -[f]x R[:, q]
+                B.b[3 + r][q] = -dta * (fs[r][0] * Rc[0 * 3 + q] + fs[r][1] * Rc[1 * 3 + q] + fs[r][2] * Rc[2 * 3 + q]);
+            B.b[3 + r][5] = dta * Rc[r * 3 + 2];   // tau
+        }
+    }
+}
+
 }  // namespace cmpc

@@ -60,6 +60,7 @@ struct cmpc_handle_s {
     bool ks_live = true;
     bool lin_lane = true;   // knot-per-lane linearization (diagonal R); else k_linearize
     bool lin_lane_done = false;   // the last linearization came from k_lin_knots (stage partly written)
+    bool lin_dense = false;       // the dense A, Bu, C arrays hold the last linearization (see ensure_dense)
     // RCCL communicator of the batch split (comm.cpp); nullptr until cmpc_comm_init
     void *comm = nullptr;
     int comm_rank = 0, comm_size = 1;

@@ -107,40 +107,8 @@ __device__ __forceinline__ void atma(const T (&M)[45], T beta, const T (&Wm)[3][
         }
 }
 
-// rows 3..8 of the per-contact input matrix B_c (6 x NUPC) of contact c
-template <typename T, int ROBOT> struct ContactB {
-    static constexpr int NUPC = Robot<ROBOT>::NUPC;
-    T b[6][NUPC];
-};
-
 template <typename T, int ROBOT>
-__device__ __forceinline__ void contact_B(T dta, const T (&lev)[3], const T *f, const T *Rc, ContactB<T, ROBOT> &B) {
-    constexpr int NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
-    const T sk[3][3] = {{T(0), -lev[2], lev[1]}, {lev[2], T(0), -lev[0]}, {-lev[1], lev[0], T(0)}};
-#pragma unroll
-    for (int a = 0; a < 6; ++a)
-#pragma unroll
-        for (int q = 0; q < NUPC; ++q) B.b[a][q] = T(0);
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-        B.b[q][FO + q] = dta;
-#pragma unroll
-        for (int r = 0; r < 3; ++r) B.b[3 + r][FO + q] = dta * sk[r][q];
-    }
-    if (ROBOT == 1) {
-        const T fs[3][3] = {{T(0), -f[2], f[1]}, {f[2], T(0), -f[0]}, {-f[1], f[0], T(0)}};
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-#pragma unroll
-            for (int q = 0; q < 2; ++q)   // d/dcop [(R2 cop) x f] = -[f]x R[:, q]
-                B.b[3 + r][q] = -dta * (fs[r][0] * Rc[0 * 3 + q] + fs[r][1] * Rc[1 * 3 + q] + fs[r][2] * Rc[2 * 3 + q]);
-            B.b[3 + r][5] = dta * Rc[r * 3 + 2];   // tau
-        }
-    }
-}
-
-template <typename T, int ROBOT>
-__global__ void __launch_bounds__(256, 1) k_lin_knots(DevBuf<T> d, int only_active) {
+__global__ void __launch_bounds__(256, 1) k_lin_knots(DevBuf<T> d, int only_active, int dense) {
     constexpr int NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO, NW = 3 * NC;
     const int N = d.N;
     const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -206,8 +174,10 @@ __global__ void __launch_bounds__(256, 1) k_lin_knots(DevBuf<T> d, int only_acti
         for (int i = 0; i < 9; ++i) em(d.f, i) = fx[i];
     }
     const T Wm[3][3] = {{T(0), -dt * w[2], dt * w[1]}, {dt * w[2], T(0), -dt * w[0]}, {-dt * w[1], dt * w[0], T(0)}};
-    // ---- A, B, C (jacfwd at :230-232), closed form
-    // ---- A, B, C (jacfwd at :230-232) and the linearization part of the stage record
+    // ---- A, B, C (jacfwd at :230-232), closed form, and the linearization part of the stage record.
+    // The dense A, B, C are stored only with `dense` (GuSTO mode, or on demand for the getters): the
+    // QP takes its dynamics from the stage record and k_accept's linear prediction recomputes the
+    // same closed form, so in reference mode the SCP loop never reads them.
     {
 #pragma unroll
         for (int i = 0; i < 9; ++i)
@@ -216,7 +186,7 @@ __global__ void __launch_bounds__(256, 1) k_lin_knots(DevBuf<T> d, int only_acti
                 T v = (i == j) ? T(1) : T(0);
                 if (i < 3 && j == i + 3) v = beta;
                 if (i >= 6 && j < 3) v = Wm[i - 6][j];
-                em(d.A, i * 9 + j) = v;
+                if (dense) em(d.A, i * 9 + j) = v;
             }
         // r_k = A xbar + B ubar - f (src/constraints.py:36-45)
         T r[9];
@@ -235,7 +205,8 @@ __global__ void __launch_bounds__(256, 1) k_lin_knots(DevBuf<T> d, int only_acti
 #pragma unroll
             for (int i = 0; i < 9; ++i)
 #pragma unroll
-                for (int q = 0; q < NUPC; ++q) em(d.Bu, i * NU + NUPC * c + q) = i < 3 ? T(0) : Bc.b[i - 3][q];
+                for (int q = 0; q < NUPC; ++q)
+                    if (dense) em(d.Bu, i * NU + NUPC * c + q) = i < 3 ? T(0) : Bc.b[i - 3][q];
 #pragma unroll
             for (int i = 0; i < 6; ++i)
 #pragma unroll
@@ -245,7 +216,8 @@ __global__ void __launch_bounds__(256, 1) k_lin_knots(DevBuf<T> d, int only_acti
 #pragma unroll
             for (int i = 0; i < 9; ++i)
 #pragma unroll
-                for (int q = 0; q < 3; ++q) em(d.C, i * NW + 3 * c + q) = i < 6 ? T(0) : -dt * a[c] * fs[i - 6][q];
+                for (int q = 0; q < 3; ++q)
+                    if (dense) em(d.C, i * NW + 3 * c + q) = i < 6 ? T(0) : -dt * a[c] * fs[i - 6][q];
             // per-contact stage fields: alpha, lever, friction rows (F_mu R')[0:4], TALOS cop / tau columns
             const SV<T> cs = st + (St::CON + St::CS * c);
             cs[St::ALPHA] = dt * a[c];
@@ -495,7 +467,7 @@ template <typename T, int ROBOT> __global__ void __launch_bounds__(64, 4) k_cov_
 }
 
 #define INST(T, R)                                                     \
-    template __global__ void k_lin_knots<T, R>(DevBuf<T>, int);      \
+    template __global__ void k_lin_knots<T, R>(DevBuf<T>, int, int); \
     template __global__ void k_cov_scan<T, R>(DevBuf<T>, int);
 INST(double, 0)
 INST(double, 1)

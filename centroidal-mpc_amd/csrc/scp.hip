@@ -134,6 +134,46 @@ __device__ void step_dyn(const DevParams<T> &prm, const T *x, const T *u, const 
 constexpr int ACC_NT = 64;
 constexpr int ACC_KC = 128, ACC_REC = 9 + 9 + NU;   // knots per rho chunk, LDS record per knot
 
+// Linear prediction f + A dx + B du of knot kn (compute_model_accuracy, src/scp_solver.py:71-87),
+// with A and B at the linearization point (xb, ub) in the closed form k_lin_knots uses
+// (src/centroidal_model.py:230-232): A = [[I, beta I, 0], [0, I, 0], [[dt w]x, 0, I]], B from
+// contact_B.  The sum runs in the dense product's order over its nonzero entries (a zero entry's
+// fma is an exact no-op), so the prediction is bit-identical to f + A dx + B du with the dense
+// arrays, which reference mode no longer stores.
+template <typename T, int ROBOT>
+__device__ __forceinline__ void lin_predict(const DevBuf<T> &d, const DevParams<T> &prm, size_t kn, const T *xb, const T *ub,
+                                            const T *xs, const T *us, T *lin) {
+    constexpr int NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
+    T x[9], u[NU], dx[9], du[NU];
+    for (int i = 0; i < 9; ++i) { x[i] = xb[i]; dx[i] = xs[i] - x[i]; }
+    for (int i = 0; i < NU; ++i) { u[i] = ub[i]; du[i] = us[i] - u[i]; }
+    const T *p = d.pos + kn * 3 * NC, *rot = d.rot + kn * 9 * NC;
+    T a[NC], lev[NC][3], w[3] = {T(0), T(0), T(0)};
+    for (int c = 0; c < NC; ++c) a[c] = T(d.logic[kn * NC + c]);
+    for (int c = 0; c < NC; ++c)
+        for (int z = 0; z < 3; ++z) {
+            lev[c][z] = p[3 * c + z] - x[z];
+            if (ROBOT == 1) lev[c][z] += rot[9 * c + z * 3] * u[NUPC * c] + rot[9 * c + z * 3 + 1] * u[NUPC * c + 1];
+            w[z] = fma(a[c], u[NUPC * c + FO + z], w[z]);
+        }
+    const T dt = prm.dt, beta = dt / prm.mass;
+    const T Wm[3][3] = {{T(0), -dt * w[2], dt * w[1]}, {dt * w[2], T(0), -dt * w[0]}, {-dt * w[1], dt * w[0], T(0)}};
+    for (int i = 0; i < 9; ++i) lin[i] = d.f[(size_t)i * d.LS + kn];
+    for (int i = 0; i < 3; ++i) lin[i] = fma(beta, dx[3 + i], lin[i] + dx[i]);     // j = i, then j = i + 3
+    for (int i = 3; i < 6; ++i) lin[i] = lin[i] + dx[i];
+    for (int i = 6; i < 9; ++i) {
+        T v = lin[i];
+        for (int j = 0; j < 3; ++j) v = fma(Wm[i - 6][j], dx[j], v);              // j < 3, then j = i
+        lin[i] = v + dx[i];
+    }
+    for (int c = 0; c < NC; ++c) {
+        ContactB<T, ROBOT> Bc;
+        contact_B<T, ROBOT>(dt * a[c], lev[c], u + NUPC * c + FO, rot + 9 * c, Bc);
+        for (int i = 3; i < 9; ++i)
+            for (int q = 0; q < NUPC; ++q) lin[i] = fma(Bc.b[i - 3][q], du[NUPC * c + q], lin[i]);
+    }
+}
+
 template <typename T, int ROBOT>
 __global__ void __launch_bounds__(ACC_NT) k_accept(DevBuf<T> d, int fixed_iters) {
     constexpr int NC = Robot<ROBOT>::NC;
@@ -164,21 +204,17 @@ __global__ void __launch_bounds__(ACC_NT) k_accept(DevBuf<T> d, int fixed_iters)
         for (int kk = tid; kk < nk; kk += ACC_NT) {
             const int k = k0 + kk;
             const size_t kn = (size_t)b * N + k;
-            T *rec = acc_sm + kk * ACC_REC;   // nl (9) | dx (9) | du (NU)
+            T *rec = acc_sm + kk * ACC_REC;   // nl (9) | lin (9)
             step_dyn<T, ROBOT>(prm, Xs + (size_t)k * 9, Us + (size_t)k * NU, d.pos + kn * 3 * NC, d.rot + kn * 9 * NC,
                                d.logic + kn * NC, rec);
-            for (int i = 0; i < 9; ++i) rec[9 + i] = Xs[(size_t)k * 9 + i] - Xb[(size_t)k * 9 + i];
-            for (int i = 0; i < NU; ++i) rec[18 + i] = Us[(size_t)k * NU + i] - Ub[(size_t)k * NU + i];
+            lin_predict<T, ROBOT>(d, prm, kn, Xb + (size_t)k * 9, Ub + (size_t)k * NU, Xs + (size_t)k * 9,
+                                  Us + (size_t)k * NU, rec + 9);
         }
         __syncthreads();
         for (int p = tid; p < nk * 9; p += ACC_NT) {
-            const int kk = p % nk, i = p / nk;   // neighbouring threads: neighbouring knots (element-major arrays)
-            const size_t kn = (size_t)b * N + k0 + kk;
+            const int kk = p % nk, i = p / nk;
             const T *rec = acc_sm + kk * ACC_REC;
-            const T *Ar = d.A + (size_t)(i * 9) * d.LS + kn, *Br = d.Bu + (size_t)(i * NU) * d.LS + kn;
-            T lin = d.f[(size_t)i * d.LS + kn];
-            for (int j = 0; j < 9; ++j) lin = fma(Ar[(size_t)j * d.LS], rec[9 + j], lin);
-            for (int j = 0; j < NU; ++j) lin = fma(Br[(size_t)j * d.LS], rec[18 + j], lin);
+            const T lin = rec[9 + i];
             if (i >= 6) acc[0] += sq(rec[i] - lin);
             acc[1] += lin * lin;
         }
