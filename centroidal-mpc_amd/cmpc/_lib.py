@@ -183,6 +183,7 @@ class Solver:
         self.prec = PREC[precision]
         self.max_batch = int(max_batch)
         self.B = 0
+        self._epoch = 0   # counts C-ABI calls: a cached export is valid only while no call followed it
         h = ctypes.c_void_p()
         rc = self.lib.cmpc_create(ctypes.byref(h), int(device), ROBOTS[robot], self.N, self.max_batch, self.prec)
         if rc != 0 or not h.value:
@@ -190,6 +191,7 @@ class Solver:
         self.h = h
 
     def _chk(self, rc, what):
+        self._epoch += 1
         if rc != 0:
             msg = self.lib.cmpc_last_error(self.h)
             raise CmpcError('%s failed (rc=%d): %s' % (what, rc, msg.decode() if msg else ''))

@@ -5,20 +5,46 @@ form; ``cmpc_export_qp`` writes it out as CSC in the reference's exact variable 
 (z = [x | u | t | s], rows init | dyn | final | [cop] | friction | trust region | slack), which
 is how the reference's matrix-building functions are answered here.
 """
+import hashlib
+
 import numpy as np
+
+
+def _key(model, traj_tuple, trust_region):
+    """What the exported QP depends on: the linearization point's content (not the dict's
+    identity: a caller may edit the arrays in place) and the trust-region weight and radius."""
+    traj = model._init_trajectories if traj_tuple is None else traj_tuple
+    h = hashlib.blake2b(digest_size=16)
+    for k in ('state', 'control'):
+        h.update(np.ascontiguousarray(np.asarray(traj[k], float)).tobytes())
+    tr = None if trust_region is None else (float(np.asarray(trust_region['weight'])),
+                                            float(np.asarray(trust_region['radius'])))
+    return h.digest(), tr
 
 
 def export(model, traj_tuple=None, trust_region=None):
     """(solver, P, q, A, l, u) for ``model`` linearized at ``traj_tuple`` (default: the model's
-    warm start) with ``trust_region`` = {'weight', 'radius'} (default omega0 / radius0)."""
+    warm start) with ``trust_region`` = {'weight', 'radius'} (default omega0 / radius0).
+
+    The reference's solve_scp asks for the cost and for each constraint family of the same QP
+    separately (src/scp_solver.py:10-48), so the last export is kept: a call for the same
+    linearization point and trust region reuses it instead of linearizing, assembling and
+    downloading again.  Any other device call on the model's handle drops it."""
+    key = _key(model, traj_tuple, trust_region)
+    hit = getattr(model, '_export_cache', None)
+    if hit is not None and hit[0] == key and hit[1] is model._solver and model._solver is not None \
+            and model._solver._epoch == hit[2]:
+        s, *arrs = hit[3]
+        return (s,) + tuple(a.copy() for a in arrs)   # copies: a caller may edit what it got
     s = model._device_solver(traj_tuple)
     if trust_region is not None:
-        s.set_trust_region(weight=float(np.asarray(trust_region['weight'])),
-                           radius=float(np.asarray(trust_region['radius'])))
+        s.set_trust_region(weight=key[1][0], radius=key[1][1])
     s.linearize()
     s.assemble()
     P, q, A, l, u = s.export_qp(0)
-    return s, P, q, A, l, u
+    out = (s, P, q, A, l, u)
+    model._export_cache = (key, s, s._epoch, (s,) + tuple(a.copy() for a in out[1:]))
+    return out
 
 
 def row_blocks(model):

@@ -114,3 +114,19 @@ def test_foreign_qp_layout_inference_rejects_other_sizes():
         _foreign_solver(23 * 30 + 11, 38 * 30 + 27)
     with pytest.raises(ValueError, match='rows'):
         _foreign_solver(23 * 30 + 10, 38 * 30 + 28)
+
+
+def test_export_cache_key_follows_content_and_trust_region():
+    """The drop-in keeps the last exported QP (the reference asks for the cost and every
+    constraint family of one QP separately); its key is the linearization point's content and
+    the trust region, so an in-place edit or another radius is a different QP."""
+    m = dropin_model('trot', 20)
+    tr = {'weight': 100.0, 'radius': 100.0}
+    k0 = _device._key(m, None, tr)
+    assert _device._key(m, None, dict(tr)) == k0
+    assert _device._key(m, None, {'weight': 100.0, 'radius': 50.0}) != k0
+    traj = {k: np.array(v, copy=True) for k, v in m._init_trajectories.items()}
+    assert _device._key(m, traj, tr) == k0
+    traj['state'][3, 7] += 1e-9
+    assert _device._key(m, traj, tr) != k0
+    m.close()

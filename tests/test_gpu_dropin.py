@@ -62,6 +62,10 @@ def test_cost_constraints_and_subproblem(cfg):
     assert cons.mat.shape == A0.shape and abs(cons.mat - A0).max() <= 1e-13
     fin = np.isfinite(u0)
     assert np.array_equal(fin, np.isfinite(cons.ub)) and np.allclose(cons.ub[fin], u0[fin], rtol=0, atol=1e-11)
+    # the same QP asked again is served from the drop-in's last export: no device call
+    ep = m._solver._epoch
+    cons2 = S.stack_up_all_constraints(m, {k: np.array(v, copy=True) for k, v in m._init_trajectories.items()}, None, tr)
+    assert m._solver._epoch == ep and abs(cons2.mat - cons.mat).max() == 0 and np.array_equal(cons2.ub, cons.ub)
     # the per-family functions stack up to the same matrix
     fams = [Cn.construct_initial_constraints(m), Cn.construct_dynamics_constraints(m, m._init_trajectories, None),
             Cn.construct_final_constraints(m)]
