@@ -188,6 +188,10 @@ int cmpc_solve_scp(cmpc_handle h, int fixed_iters, int *n_iterations_out);
 int cmpc_synchronize(cmpc_handle h);
 
 /* ---- getters (synchronous; NULL pointers are skipped) ---- */
+/* The last linearization (knot-major).  In reference mode the SCP loop does not store the dense
+ * A, Bu, C (the QP reads the stage record, the accept step the closed form); this getter and
+ * cmpc_export_qp first recompute them with one more k_lin_knots pass, which rewrites identical
+ * values because the linearization point never moves there (quirk Q1). */
 int cmpc_get_linearization(cmpc_handle h, double *f, double *A, double *Bu, double *C, double *K,
                            double *Sigma);
 int cmpc_qp_sizes(cmpc_handle h, int32_t *n, int32_t *m, int32_t *nnzP, int32_t *nnzA);
@@ -210,6 +214,10 @@ int cmpc_get_qp_solution(cmpc_handle h, double *z, double *y, int32_t *status, i
 /* Per-problem exit data of the last QP solve: final merit (<= 1 when solved) and the number of
  * iterative-refinement steps taken (B entries each; NULL skips). */
 int cmpc_get_qp_info(cmpc_handle h, double *merit, int32_t *n_refine);
+/* The accepted iterate of each problem (X, U) with that iteration's LQR gains and covariances.
+ * Reference mode serves K and Sigma from the live linearization arrays, which every iteration
+ * recomputes bit-identically (quirk Q1; the reference keeps references to that iteration's
+ * arrays).  GuSTO mode and new contact plans copy them per accept. */
 int cmpc_get_solution(cmpc_handle h, double *X, double *U, double *K, double *Sigma, int32_t *n_accepted,
                       int32_t *iterations, int32_t *scp_status, double *weight, double *radius);
 int cmpc_get_iteration_log(cmpc_handle h, double *tr_norm, double *rho, int32_t *qp_status,
