@@ -1010,7 +1010,7 @@ __device__ __forceinline__ void tw_step(const LdsT<T> *Dn, const LdsT<T> *Op, co
 // element reads A[i][c] = U[min(i,c)][max(i,c)] and A[c][j] = (c > j ? -1 : 1) U[min][max] from
 // the stored upper triangle U.  The inverse is mirrored into P (full, for the next step) and
 // stored packed into Iout.
-template <typename T>
+template <typename T, int L>
 __device__ __forceinline__ void tw_step_sym(const LdsT<T> *Dn, const LdsT<T> *Op, const LdsT<T> *Ip, GlbT<T> *Xout, GlbT<T> *Iout,
                                             LdsT<T> *A, LdsT<T> *P, LdsT<T> *Xb, LdsT<T> *Dd, LdsT<T> *vb, int j,
                                             int jx, unsigned long long *sub = nullptr) {
@@ -1020,24 +1020,25 @@ __device__ __forceinline__ void tw_step_sym(const LdsT<T> *Dn, const LdsT<T> *Op
 #else
 #define SUBSTAMP(i) do { } while (0)
 #endif
-    const int l = threadIdx.x & 31;
-    // X elements (all 81): e = l + 32 q, clamped to 80 past the end (bit-identical duplicates)
-    int e[3], ii[3], cc[3];
-    bool ok[3];
+    constexpr int NX = (81 + L - 1) / L, NU2 = (45 + L - 1) / L;   // X / upper-triangle elements per lane
+    const int l = threadIdx.x & (L - 1);
+    // X elements (all 81): e = l + L q, clamped to 80 past the end (bit-identical duplicates)
+    int e[NX], ii[NX], cc[NX];
+    bool ok[NX];
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
-        ok[q] = l + 32 * q < 81;
-        e[q] = ok[q] ? l + 32 * q : 80;
+    for (int q = 0; q < NX; ++q) {
+        ok[q] = l + L * q < 81;
+        e[q] = ok[q] ? l + L * q : 80;
         ii[q] = e[q] / 9;
         cc[q] = e[q] % 9;
     }
-    // upper-triangle elements u = l + 32 q (row-major over i <= j), clamped to 44 = (8, 8)
-    int iu[2], ju[2];
-    bool oku[2];
+    // upper-triangle elements u = l + L q (row-major over i <= j), clamped to 44 = (8, 8)
+    int iu[NU2], ju[NU2];
+    bool oku[NU2];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        oku[q] = l + 32 * q < 45;
-        int r = oku[q] ? l + 32 * q : 44, row = 0;
+    for (int q = 0; q < NU2; ++q) {
+        oku[q] = l + L * q < 45;
+        int r = oku[q] ? l + L * q : 44, row = 0;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {   // walk the rows (lengths 9, 8, ..., 1)
             const bool past = r >= 9 - i && row == i;
@@ -1047,9 +1048,9 @@ __device__ __forceinline__ void tw_step_sym(const LdsT<T> *Dn, const LdsT<T> *Op
         iu[q] = row;
         ju[q] = row + r;
     }
-    T au[2];
+    T au[NU2];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < NU2; ++q) {
         au[q] = Dn[iu[q] * 9 + ju[q]];
         if (iu[q] == ju[q]) Dd[iu[q]] = au[q];   // original diagonal (pivot floor)
     }
@@ -1064,31 +1065,31 @@ __device__ __forceinline__ void tw_step_sym(const LdsT<T> *Dn, const LdsT<T> *Op
         return s0 + s1 + s2;
     };
     if (Op) {   // X = Op' I_{j-1} (whole);  A -= X Op (upper triangle)
-        T x[3];
+        T x[NX];
 #pragma unroll
-        for (int q = 0; q < 3; ++q)
+        for (int q = 0; q < NX; ++q)
             x[q] = dot([&](int m) { return Op[m * 9 + ii[q]]; }, [&](int m) { return Ip[m * 9 + cc[q]]; });
 #pragma unroll
-        for (int q = 0; q < 3; ++q) Xb[e[q]] = x[q];
+        for (int q = 0; q < NX; ++q) Xb[e[q]] = x[q];
         wave_sync();
         if (vb && l < 9) rv -= dot9(Xb + l * 9, vb + jx * 9);
 #pragma unroll
-        for (int q = 0; q < 2; ++q)
+        for (int q = 0; q < NU2; ++q)
             au[q] -= dot([&](int m) { return Xb[iu[q] * 9 + m]; }, [&](int m) { return Op[m * 9 + ju[q]]; });
 #pragma unroll
-        for (int q = 0; q < 3; ++q)
+        for (int q = 0; q < NX; ++q)
             if (ok[q]) Xout[e[q]] = x[q];
     }
 #pragma unroll
-    for (int q = 0; q < 2; ++q) A[iu[q] * 9 + ju[q]] = au[q];
+    for (int q = 0; q < NU2; ++q) A[iu[q] * 9 + ju[q]] = au[q];
     wave_sync();
     SUBSTAMP(0);
     T ip = rcp_nr(fmax(A[0], T(1e-13) * Dd[0]));
 #pragma unroll
     for (int c = 0; c < 9; ++c) {
-        T aic[2], acj[2];
+        T aic[NU2], acj[NU2];
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
+        for (int q = 0; q < NU2; ++q) {
             const int i = iu[q], jj = ju[q];
             const T v1 = A[min(i, c) * 9 + max(i, c)], v2 = A[min(c, jj) * 9 + max(c, jj)];
             aic[q] = v1;
@@ -1100,7 +1101,7 @@ __device__ __forceinline__ void tw_step_sym(const LdsT<T> *Dn, const LdsT<T> *Op
             ipn = rcp_nr(fmax(fma(-(nci * ip), nci, ncc), T(1e-13) * Dd[c + 1]));
         }
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
+        for (int q = 0; q < NU2; ++q) {
             const T mi = aic[q] * ip;
             const T gen = fma(-mi, acj[q], au[q]), row = acj[q] * ip, col = -mi;
             const bool ic = __builtin_unpredictable(iu[q] == c), jc = __builtin_unpredictable(ju[q] == c);
@@ -1108,13 +1109,13 @@ __device__ __forceinline__ void tw_step_sym(const LdsT<T> *Dn, const LdsT<T> *Op
         }
         wave_sync();
 #pragma unroll
-        for (int q = 0; q < 2; ++q) A[iu[q] * 9 + ju[q]] = au[q];
+        for (int q = 0; q < NU2; ++q) A[iu[q] * 9 + ju[q]] = au[q];
         wave_sync();
         ip = ipn;
     }
     SUBSTAMP(1);
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < NU2; ++q) {
         P[iu[q] * 9 + ju[q]] = au[q];
         P[ju[q] * 9 + iu[q]] = au[q];
         if (oku[q]) Iout[ju[q] * (ju[q] + 1) / 2 + iu[q]] = au[q];   // packed (row ju >= column iu)
@@ -1125,18 +1126,20 @@ __device__ __forceinline__ void tw_step_sym(const LdsT<T> *Dn, const LdsT<T> *Op
 #undef SUBSTAMP
 }
 
-// the two ends, one per half-wave: lanes 0..31 the top blocks 0..m-1, lanes 32..63 the bottom
-// blocks NB-1..m+1 (for even NB the top end has one step more; the bottom half idles in it).
+// the two ends, one per group of L lanes: with one wave per problem (L = 32) lanes 0..31 the top
+// blocks 0..m-1 and lanes 32..63 the bottom blocks NB-1..m+1; with two waves per problem (L = 64)
+// wave 0 the top and wave 1 the bottom, so every step has half the elements per lane (for even
+// NB the top end has one step more; the bottom group idles in it).
 // The raw blocks of step s + 1 are loaded during step s and landed in LDS at its end, inside
 // the same loop iteration: registers carried over the back-edge with loads in flight would make
 // the compiler drain the whole memory queue (this step's stores included) at the loop header.
 // The bottom end lands its coupling block S_{j,j+1} transposed, so both ends run the same step.
-template <typename T>
+template <typename T, int L>
 __device__ void tw_factor_ends(T *Sd_, T *So_, int NB, int m, LdsT<T> *sh, LdsT<T> *vb, unsigned long long *stamp_out) {
     GlbT<T> *Sd = (GlbT<T> *)Sd_, *So = (GlbT<T> *)So_;
-    constexpr int NE = 3;
-    const int lane = threadIdx.x & 63, l = lane & 31;
-    const bool top = lane < 32;
+    constexpr int NE = (81 + L - 1) / L;
+    const int l = threadIdx.x & (L - 1);
+    const bool top = (threadIdx.x & L) == 0;
     LdsT<T> *A = sh + (top ? 0 : TW_SCRATCH), *P = A + 88, *Xb = A + 176, *Ob = A + 264, *Dd = A + 352,
             *Dn = A + 368;
     const int j0 = top ? 0 : NB - 1, dj = top ? 1 : -1, nstep = top ? m : NB - 1 - m;
@@ -1145,8 +1148,8 @@ __device__ void tw_factor_ends(T *Sd_, T *So_, int NB, int m, LdsT<T> *sh, LdsT<
     T em[NE];
 #pragma unroll
     for (int q = 0; q < NE; ++q) {
-        ok[q] = l + 32 * q < 81;
-        e[q] = ok[q] ? l + 32 * q : 80;
+        ok[q] = l + L * q < 81;
+        e[q] = ok[q] ? l + L * q : 80;
         et[q] = top ? e[q] : (e[q] % 9) * 9 + e[q] / 9;   // landing slot of a coupling element
         ep[q] = pk9(e[q] / 9, e[q] % 9);                   // packed slot of a diagonal-block element
         const int c = cp9(e[q] / 9, e[q] % 9);            // compact slot of a coupling element
@@ -1174,9 +1177,9 @@ __device__ void tw_factor_ends(T *Sd_, T *So_, int NB, int m, LdsT<T> *sh, LdsT<
         for (int q = 0; q < NE; ++q) { pv[q] = On[ec[q]] * em[q]; nv[q] = Dnx[ep[q]]; }
         if (act) {
             if (s == 0)
-                tw_step_sym<T>(Dn, nullptr, nullptr, nullptr, Sd + (size_t)j * 81, A, P, Xb, Dd, vb, j, 0, subp);
+                tw_step_sym<T, L>(Dn, nullptr, nullptr, nullptr, Sd + (size_t)j * 81, A, P, Xb, Dd, vb, j, 0, subp);
             else
-                tw_step_sym<T>(Dn, Ob, P, So + (size_t)(top ? j - 1 : j) * 81, Sd + (size_t)j * 81, A, P, Xb, Dd, vb,
+                tw_step_sym<T, L>(Dn, Ob, P, So + (size_t)(top ? j - 1 : j) * 81, Sd + (size_t)j * 81, A, P, Xb, Dd, vb,
                                j, j - dj, subp);
         }
 #ifdef CMPC_STAMPS
@@ -1189,7 +1192,7 @@ __device__ void tw_factor_ends(T *Sd_, T *So_, int NB, int m, LdsT<T> *sh, LdsT<
         if (subp) sub[3] += __builtin_amdgcn_s_memtime() - tl;
 #endif
     }
-    if (stamp_out && lane == 0)
+    if (stamp_out && top && l == 0)
         for (int i = 0; i < 4; ++i) stamp_out[12 + i] += sub[i];
 }
 
@@ -2084,12 +2087,15 @@ __global__ void __launch_bounds__(NTT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int o
         __syncthreads();
         STAMP(2);
         // ---- factorization of S with the predictor's forward elimination fused in
-        if (tid < 64) {   // the recurrence runs on wave 0 (the other waves wait at the barrier)
 #ifdef CMPC_STAMPS
-            tw_factor_ends<T>(C.Sd, C.So, NB, NBm, shl, C.vb, d.stamps + (size_t)b * 16);
+        unsigned long long *fst = d.stamps + (size_t)b * 16;
 #else
-            tw_factor_ends<T>(C.Sd, C.So, NB, NBm, shl, C.vb, nullptr);
+        unsigned long long *fst = nullptr;
 #endif
+        if (NTT >= 128) {   // one end per wave (waves 0 and 1; any further waves wait at the barrier)
+            if (tid < 128) tw_factor_ends<T, 64>(C.Sd, C.So, NB, NBm, shl, C.vb, fst);
+        } else {            // one end per half of wave 0
+            tw_factor_ends<T, 32>(C.Sd, C.So, NB, NBm, shl, C.vb, fst);
         }
         __syncthreads();
         if (tid < 64) tw_factor_meet<T>(C.Sd, C.So, NBm, shl, C.vb);
