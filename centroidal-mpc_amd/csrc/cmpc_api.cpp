@@ -326,7 +326,7 @@ int cmpc_default_qp_settings(int precision, cmpc_qp_settings *s) {
     s->max_iter = precision == CMPC_PREC_F64 ? 60 : 40;
     s->eps_abs = precision == CMPC_PREC_F64 ? 1e-10 : 1e-6;
     s->eps_rel = precision == CMPC_PREC_F64 ? 1e-10 : 1e-6;
-    s->step_fraction = 0.995;   // 0.99 -> 0.995: trot N=100 x 1024 5.24 -> 4.81 Newton steps (profiles/r02_eta_sweep.log)
+    s->step_fraction = 0.999;   // 0.99 -> 0.995 -> 0.999: trot N=100 x 1024 5.24 -> 4.81 -> 4.67 Newton steps (profiles/r02_eta_sweep*.log)
     s->init_floor_s = 0.1;
     s->init_floor_l = 0.1;
     s->waves_per_problem = 0;

@@ -83,7 +83,7 @@ INIT_FLOOR = 0.1          # s floor of the Solo12 starting point
 INIT_FLOOR_L = 0.1        # lambda floor
 
 
-def solve(qp, eps=1e-11, max_iter=60, eta=0.995, verbose=False, reg=0.0, piv_floor=1e-13, dcap_rel=1e12,
+def solve(qp, eps=1e-11, max_iter=60, eta=0.999, verbose=False, reg=0.0, piv_floor=1e-13, dcap_rel=1e12,
           refine_alpha=0.5, refine_merit=1e6, eps_pinf=1e-4, init_floor=INIT_FLOOR,
           init_floor_l=INIT_FLOOR_L, fric_floor=1e-9):
     N, nc, nu, nupc = qp.N, qp.nc, qp.nu, qp.nupc

@@ -67,3 +67,23 @@ def test_plan_validation():
         g = dict(type='PACE', nbSteps=1, stepKnots=5, supportKnots=5, stepLength=0.0)
         with pytest.raises(Exception, match='shorter than the horizon'):
             s.generate_contact_plans([g], np.zeros((1, 2, 3)))
+
+
+def test_accepted_gains_kept_across_new_plans():
+    """Reference mode serves the accepted K / Sigma from the live arrays; new contact plans change
+    what a later linearization computes, so they are copied first: after regenerating the plans
+    (a different gait) and linearizing, the accepted results still equal those of the solve."""
+    N, B = 60, 4
+    pb = make_batch('trot', N, B)
+    gaits, feet = _specs(['bound'], N, B)
+    with Solver(pb.robot, N, B, 'fp64') as s:
+        s.upload(pb)
+        s.solve_scp(fixed_iters=False)
+        sol = s.solution()
+        assert np.all(sol['n_accepted'] >= 1)
+        s.generate_contact_plans(gaits, feet)
+        s.linearize()
+        after = s.solution()
+        np.testing.assert_array_equal(after['K'], sol['K'])
+        np.testing.assert_array_equal(after['Sigma'], sol['Sigma'])
+        assert not np.array_equal(s.linearization()['K'], sol['K'])   # the live arrays did change
