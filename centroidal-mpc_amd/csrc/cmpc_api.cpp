@@ -103,6 +103,15 @@ int qp_waves(cmpc_handle h) {
     return (h->N + 1 > 64 && 2L * h->B <= 4L * h->n_cu) ? 2 : 1;
 }
 
+// QP step fraction: the setting, or (0) the robot's. Same-box A/B, bench lines A B A B:
+// Solo12 trot N=100 x 1024 0.995 -> 0.999 316.8k -> 319.5k SCP it/s, 4.81 -> 4.67 Newton steps
+// (profiles/r02_eta999_ab.jsonl); TALOS N=200 x 512 0.999 -> 0.995 56.2k -> 59.4k
+// (profiles/r02_talos_eta_ab.jsonl).
+double qp_step_fraction(cmpc_handle h) {
+    if (h->qs.step_fraction > 0) return h->qs.step_fraction;
+    return h->robot == 1 ? 0.995 : 0.999;
+}
+
 template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int only_active) {
     DevBuf<T> d = h->buf<T>();
     const int B = h->B;
@@ -141,17 +150,18 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
         // one workgroup per problem (one or two waves, cmpc_qp_settings::waves_per_problem); the
         // (N+2) x 9 Schur vector and the sweep rings in LDS, the Schur blocks in the workspace
         const int nt = 64 * qp_waves(h);
+        const T eta = T(qp_step_fraction(h));
         const size_t lds = ipm_lds_bytes(h->N, (int)sizeof(T), nt);
         const void *fn = nt == 128 ? reinterpret_cast<const void *>(&k_qp_ipm<T, R, 128>)
                                    : reinterpret_cast<const void *>(&k_qp_ipm<T, R, 64>);
         HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         if (nt == 128)
             hipLaunchKernelGGL((k_qp_ipm<T, R, 128>), dim3(B), dim3(128), lds, h->stream, d, only_active,
-                               h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), T(h->qs.step_fraction),
+                               h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), eta,
                                T(h->qs.init_floor_s), T(h->qs.init_floor_l));
         else
             hipLaunchKernelGGL((k_qp_ipm<T, R, 64>), dim3(B), dim3(64), lds, h->stream, d, only_active,
-                               h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), T(h->qs.step_fraction),
+                               h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), eta,
                                T(h->qs.init_floor_s), T(h->qs.init_floor_l));
         break;
     }
@@ -326,7 +336,7 @@ int cmpc_default_qp_settings(int precision, cmpc_qp_settings *s) {
     s->max_iter = precision == CMPC_PREC_F64 ? 60 : 40;
     s->eps_abs = precision == CMPC_PREC_F64 ? 1e-10 : 1e-6;
     s->eps_rel = precision == CMPC_PREC_F64 ? 1e-10 : 1e-6;
-    s->step_fraction = 0.999;   // 0.99 -> 0.995 -> 0.999: trot N=100 x 1024 5.24 -> 4.81 -> 4.67 Newton steps (profiles/r02_eta_sweep*.log)
+    s->step_fraction = 0.0;     // the robot's default, qp_step_fraction
     s->init_floor_s = 0.1;
     s->init_floor_l = 0.1;
     s->waves_per_problem = 0;
@@ -418,7 +428,7 @@ int cmpc_destroy(cmpc_handle h) {
 
 int cmpc_set_qp_settings(cmpc_handle h, const cmpc_qp_settings *s) {
     return guard(h, [&] {
-        need(s && s->max_iter > 0 && s->step_fraction > 0 && s->step_fraction < 1 && s->init_floor_s >= 0 &&
+        need(s && s->max_iter > 0 && s->step_fraction >= 0 && s->step_fraction < 1 && s->init_floor_s >= 0 &&
                  s->init_floor_l >= 0 && (s->init_floor_s > 0) == (s->init_floor_l > 0) && s->waves_per_problem >= 0 &&
                  s->waves_per_problem <= 2, "invalid QP settings");
         h->qs = *s;

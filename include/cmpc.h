@@ -104,7 +104,8 @@ typedef struct {
     int32_t max_iter;       /* interior-point iterations (default 60) */
     double eps_abs;         /* absolute tolerance (fp64 default 1e-10, fp32 1e-6) */
     double eps_rel;         /* relative tolerance (fp64 default 1e-10, fp32 1e-6) */
-    double step_fraction;   /* fraction-to-boundary (default 0.999) */
+    double step_fraction;   /* fraction-to-boundary in (0, 1); 0 (default) picks the robot's:
+                             * Solo12 0.999, TALOS 0.995 (same-box measured) */
     /* Solo12 starting point: after the least-squares initialization step, s and lambda are
      * floored row by row at these values (default 0.1, 0.1); 0 selects CVXOPT's shift of every
      * row by 1 + the largest violation, which TALOS handles always use */

@@ -61,3 +61,34 @@ def test_waves_setting_is_validated():
     with pytest.raises(Exception):
         s.set_qp_settings(waves_per_problem=3)
     s.close()
+
+
+@pytest.mark.parametrize('cfg,N,eta', [('trot', 40, 0.999), ('talos', 40, 0.995)])
+def test_step_fraction_default_is_per_robot(cfg, N, eta):
+    """step_fraction 0 (the default) resolves to the robot's value (cmpc_api.cpp qp_step_fraction):
+    a default run and one with that value set explicitly are bit-identical; 0.9 differs."""
+    pb = make_batch(cfg, N, 4, seed_offset=7)
+
+    def run(**kw):
+        s = Solver(pb.robot, N, pb.B, 'fp64')
+        if kw:
+            s.set_qp_settings(**kw)
+        s.upload(pb)
+        s.scp_iterate(fixed_iters=True)
+        z, _, st, it = s.qp_solution(with_y=False)
+        s.close()
+        return z, st, it
+
+    z0, s0, i0 = run()
+    z1, s1, i1 = run(step_fraction=eta)
+    assert np.all(s0 == 1)
+    np.testing.assert_array_equal(i0, i1)
+    np.testing.assert_array_equal(z0, z1)
+    z2, _, _ = run(step_fraction=0.9)
+    assert not np.array_equal(z0, z2)
+    s = Solver(pb.robot, N, pb.B, 'fp64')
+    with pytest.raises(Exception):
+        s.set_qp_settings(step_fraction=-0.5)
+    with pytest.raises(Exception):
+        s.set_qp_settings(step_fraction=1.0)
+    s.close()
