@@ -112,10 +112,49 @@ double qp_step_fraction(cmpc_handle h) {
     return h->robot == 1 ? 0.995 : 0.999;
 }
 
-template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int only_active) {
+// Covariance scan placement.  Sigma feeds only the chance-constraint back-off of stochastic
+// problems (k_assemble) and the outputs, so inside cmpc_scp_iterate a deterministic batch runs the
+// scan on the low-priority side stream, started when the assembly ends, i.e. when the QP becomes
+// ready too: the QP's workgroups (one wave per SIMD with the whole register file) are dispatched
+// first, and the scan's waves take the SIMDs whose problems have finished their Newton steps.  The
+// main stream waits for the scan right behind the QP, so k_accept, k_keep_accepted, the getters and
+// the next linearization (which rewrites Acl / Qw) are ordered after it.
+template <typename T, int R> void launch_scan(cmpc_handle h, hipStream_t s, int only_active) {
+    hipLaunchKernelGGL((k_cov_scan<T, R>), dim3(h->B), dim3(64), 0, s, h->buf<T>(), only_active);
+}
+
+// Only where the QP leaves room: two-wave QP workgroups, or fewer QP waves than SIMDs.  With one
+// wave per SIMD over the whole device (the metric config, 1024 problems) the scan's waves delayed
+// the QP's dispatch: 318.7k -> 258.8k SCP it/s, while two-wave batches gained (C2 161.2k -> 165.5k,
+// C4 59.5k -> 60.5k; same-box A/B, profiles/r02_scan_overlap_ab.txt).
+bool scan_beside_qp(cmpc_handle h) {
+    const int w = qp_waves(h);
+    return w == 2 || (long)h->B * w < 4L * h->n_cu;
+}
+
+bool any_stochastic(cmpc_handle h) {
+    for (auto &p : h->hparams)
+        if (p.stochastic) return true;
+    return false;
+}
+
+// settle a deferred or running side-stream scan (before anything that is not assembly or QP)
+template <typename T, int R> void settle_scan(cmpc_handle h, int only_active) {
+    if (h->scan_deferred) {
+        launch_scan<T, R>(h, h->stream, only_active);
+        h->scan_deferred = false;
+    }
+    if (h->scan_pending) {
+        HIPCHK(hipStreamWaitEvent(h->stream, h->ev_scan, 0));
+        h->scan_pending = false;
+    }
+}
+
+template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int only_active, bool overlap = false) {
     DevBuf<T> d = h->buf<T>();
     const int B = h->B;
     if (B == 0) return;
+    if (phase == 0 || phase == 3) settle_scan<T, R>(h, only_active);
     switch (phase) {
     case 0:
         // one knot per lane (diagonal R; also writes the linearization part of the stage records),
@@ -134,7 +173,10 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
             h->lin_dense = true;
         }
         h->lin_lane_done = h->lin_lane;
-        hipLaunchKernelGGL((k_cov_scan<T, R>), dim3(B), dim3(64), 0, h->stream, d, only_active);
+        if (overlap && !any_stochastic(h) && scan_beside_qp(h))
+            h->scan_deferred = true;   // started behind the assembly (case 1)
+        else
+            launch_scan<T, R>(h, h->stream, only_active);
         break;
     case 1: {
         const long n = (long)B * (h->N + 1);
@@ -144,6 +186,14 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
         else
             hipLaunchKernelGGL((k_assemble<T, R, true>), dim3((unsigned)((n + 127) / 128)), dim3(128), 0, h->stream, d,
                                only_active);
+        if (h->scan_deferred) {
+            HIPCHK(hipEventRecord(h->ev_asm, h->stream));
+            HIPCHK(hipStreamWaitEvent(h->side, h->ev_asm, 0));
+            launch_scan<T, R>(h, h->side, only_active);
+            HIPCHK(hipEventRecord(h->ev_scan, h->side));
+            h->scan_deferred = false;
+            h->scan_pending = true;
+        }
         break;
     }
     case 2: {
@@ -163,6 +213,10 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
             hipLaunchKernelGGL((k_qp_ipm<T, R, 64>), dim3(B), dim3(64), lds, h->stream, d, only_active,
                                h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), eta,
                                T(h->qs.init_floor_s), T(h->qs.init_floor_l));
+        if (h->scan_pending) {   // join behind the QP
+            HIPCHK(hipStreamWaitEvent(h->stream, h->ev_scan, 0));
+            h->scan_pending = false;
+        }
         break;
     }
     case 3:
@@ -260,13 +314,15 @@ void ensure_dense(cmpc_handle h) {
     h->lin_dense = true;
 }
 
-void phase(cmpc_handle h, int ph, int only_active) {
+void phase(cmpc_handle h, int ph, int only_active, bool overlap = false) {
     need(h->B > 0, "no problems uploaded");
     need(h->n_classes > 0, "parameters not set");
     if (h->prec == CMPC_PREC_F64) {
-        if (h->robot == 0) launch_phase<double, 0>(h, ph, only_active); else launch_phase<double, 1>(h, ph, only_active);
+        if (h->robot == 0) launch_phase<double, 0>(h, ph, only_active, overlap);
+        else launch_phase<double, 1>(h, ph, only_active, overlap);
     } else {
-        if (h->robot == 0) launch_phase<float, 0>(h, ph, only_active); else launch_phase<float, 1>(h, ph, only_active);
+        if (h->robot == 0) launch_phase<float, 0>(h, ph, only_active, overlap);
+        else launch_phase<float, 1>(h, ph, only_active, overlap);
     }
 }
 
@@ -361,6 +417,11 @@ int cmpc_create(cmpc_handle *out, int device, int robot, int N, int max_batch, i
         need(device >= 0 && device < ndev, "invalid device id");
         HIPCHK(hipSetDevice(device));
         HIPCHK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+        int prio_low = 0, prio_high = 0;
+        HIPCHK(hipDeviceGetStreamPriorityRange(&prio_low, &prio_high));
+        HIPCHK(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, prio_low));
+        HIPCHK(hipEventCreateWithFlags(&h->ev_asm, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&h->ev_scan, hipEventDisableTiming));
         HIPCHK(hipDeviceGetAttribute(&h->n_cu, hipDeviceAttributeMultiprocessorCount, device));
         for (auto &e : h->ev) HIPCHK(hipEventCreate(&e));
         const size_t Bm = max_batch, K1 = N + 1, NB = N + 2, e = h->esz(), NC = h->NC;
@@ -413,6 +474,7 @@ int cmpc_create(cmpc_handle *out, int device, int robot, int N, int max_batch, i
 int cmpc_destroy(cmpc_handle h) {
     if (!h) return 0;
     (void)hipSetDevice(h->device);
+    if (h->side) (void)hipStreamSynchronize(h->side);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->comm && h->comm_free) h->comm_free(h->comm);
     for (void *p : h->allocs) (void)hipFree(p);
@@ -421,6 +483,9 @@ int cmpc_destroy(cmpc_handle h) {
         if (e) (void)hipEventDestroy(e);
     for (auto &a : h->ev_pool)
         for (auto &e : a) (void)hipEventDestroy(e);
+    if (h->ev_asm) (void)hipEventDestroy(h->ev_asm);
+    if (h->ev_scan) (void)hipEventDestroy(h->ev_scan);
+    if (h->side) (void)hipStreamDestroy(h->side);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return 0;
@@ -659,7 +724,7 @@ int cmpc_scp_iterate(cmpc_handle h, int fixed_iters) {
             ev = h->ev_pool[h->ev_used++].data();
         }
         HIPCHK(hipEventRecord(ev[0], h->stream));
-        phase(h, 0, oa);
+        phase(h, 0, oa, true);   // the covariance scan may run beside the QP (launch_phase)
         HIPCHK(hipEventRecord(ev[1], h->stream));
         phase(h, 1, oa);
         HIPCHK(hipEventRecord(ev[2], h->stream));

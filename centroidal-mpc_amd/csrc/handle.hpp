@@ -31,6 +31,12 @@ struct cmpc_handle_s {
     int NC = 4, NI = 25, SS = 160;
     int n_cu = 256;   // compute units of the device (QP waves-per-problem choice)
     hipStream_t stream = nullptr;
+    // Covariance scan beside the QP (deterministic batches inside cmpc_scp_iterate; see
+    // cmpc_api.cpp launch_phase): a low-priority side stream, the event after the assembly that
+    // starts it, and the event after the scan that the main stream waits for behind the QP.
+    hipStream_t side = nullptr;
+    hipEvent_t ev_asm = nullptr, ev_scan = nullptr;
+    bool scan_deferred = false, scan_pending = false;
     hipEvent_t ev[5] = {};
     bool timed = false;
     // accumulated timing: one 5-event record per cmpc_scp_iterate since cmpc_timing_reset

@@ -1,0 +1,45 @@
+"""GPU: the covariance scan beside the QP (cmpc_api.cpp launch_phase, scan_beside_qp).
+
+Inside cmpc_scp_iterate a deterministic batch whose QP leaves SIMDs free (two-wave workgroups, or
+fewer QP waves than SIMDs) runs k_cov_scan on a low-priority side stream, joined behind the QP.
+The phase-by-phase entry points (cmpc_linearize, cmpc_assemble, cmpc_qp_solve, cmpc_accept) keep
+the scan in order on the main stream.  Both orders must give bit-identical X, U, K and Sigma: the
+scan reads only what k_lin_knots wrote and nothing else in the step reads Sigma.  Cases: two-wave
+batch at the metric horizon (overlapped), a small one-wave batch (overlapped), the metric-size
+batch (one wave per SIMD: no overlap) and a stochastic batch (Sigma feeds the assembly: no
+overlap).
+"""
+import numpy as np
+import pytest
+
+from cmpc._lib import Solver
+from cmpc.synth import make_batch
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(pb, fused, steps=2):
+    s = Solver(pb.robot, pb.N, pb.B, 'fp64')
+    s.upload(pb)
+    for _ in range(steps):
+        if fused:
+            s.scp_iterate(fixed_iters=True)
+        else:
+            s.linearize(); s.assemble(); s.qp_solve(); s.accept(fixed_iters=True)
+    sol = s.solution()
+    lin = s.linearization()
+    s.close()
+    return sol, lin
+
+
+@pytest.mark.parametrize('cfg,N,B,stochastic', [('trot', 100, 256, False), ('trot', 40, 16, False),
+                                                ('trot', 100, 1024, False), ('trot', 60, 32, True)])
+def test_overlapped_scan_matches_in_order(cfg, N, B, stochastic):
+    pb = make_batch(cfg, N, B, stochastic=stochastic, seed_offset=11)
+    fused, lin_f = _run(pb, True)
+    plain, lin_p = _run(pb, False)
+    assert np.all(fused['status'] == plain['status'])
+    for k in ('X', 'U', 'K', 'Sigma'):
+        np.testing.assert_array_equal(fused[k], plain[k], err_msg=k)
+    np.testing.assert_array_equal(lin_f['Sigma'], lin_p['Sigma'])
+    assert np.abs(lin_f['Sigma'][:, -1]).max() > 0   # the scan ran to the last knot
