@@ -113,12 +113,15 @@ double qp_step_fraction(cmpc_handle h) {
 }
 
 // Covariance scan placement.  Sigma feeds only the chance-constraint back-off of stochastic
-// problems (k_assemble) and the outputs, so inside cmpc_scp_iterate a deterministic batch runs the
-// scan on the low-priority side stream, started when the assembly ends, i.e. when the QP becomes
-// ready too: the QP's workgroups (one wave per SIMD with the whole register file) are dispatched
-// first, and the scan's waves take the SIMDs whose problems have finished their Newton steps.  The
-// main stream waits for the scan right behind the QP, so k_accept, k_keep_accepted, the getters and
-// the next linearization (which rewrites Acl / Qw) are ordered after it.
+// problems (k_assemble) and the outputs, so inside cmpc_scp_iterate the scan of a deterministic
+// batch leaves the critical path:
+// - when the QP leaves SIMDs free (scan_beside_qp), k_cov_scan runs on the low-priority side
+//   stream, started when the assembly ends, and the main stream waits for it right behind the QP;
+// - when the QP fills the device with one wave per SIMD, a separate scan kernel's waves delay the
+//   QP's dispatch, so the QP kernel runs the scans itself: each workgroup whose problem has
+//   converged takes scan jobs from a counter (k_qp_ipm, d.scan_ctr).
+// Either way k_accept, k_keep_accepted, the getters and the next linearization (which rewrites
+// Acl / Qw) are ordered after the scans.
 template <typename T, int R> void launch_scan(cmpc_handle h, hipStream_t s, int only_active) {
     hipLaunchKernelGGL((k_cov_scan<T, R>), dim3(h->B), dim3(64), 0, s, h->buf<T>(), only_active);
 }
@@ -173,8 +176,8 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
             h->lin_dense = true;
         }
         h->lin_lane_done = h->lin_lane;
-        if (overlap && !any_stochastic(h) && scan_beside_qp(h))
-            h->scan_deferred = true;   // started behind the assembly (case 1)
+        if (overlap && !any_stochastic(h))
+            h->scan_deferred = true;   // beside the QP (case 1) or inside it (case 2)
         else
             launch_scan<T, R>(h, h->stream, only_active);
         break;
@@ -186,7 +189,7 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
         else
             hipLaunchKernelGGL((k_assemble<T, R, true>), dim3((unsigned)((n + 127) / 128)), dim3(128), 0, h->stream, d,
                                only_active);
-        if (h->scan_deferred) {
+        if (h->scan_deferred && scan_beside_qp(h)) {
             HIPCHK(hipEventRecord(h->ev_asm, h->stream));
             HIPCHK(hipStreamWaitEvent(h->side, h->ev_asm, 0));
             launch_scan<T, R>(h, h->side, only_active);
@@ -205,6 +208,12 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
         const void *fn = nt == 128 ? reinterpret_cast<const void *>(&k_qp_ipm<T, R, 128>)
                                    : reinterpret_cast<const void *>(&k_qp_ipm<T, R, 64>);
         HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        if (h->scan_deferred) {   // the scans run in the QP's workgroups (one-wave kernel only)
+            need(nt == 64, "internal: QP scan jobs need the one-wave kernel");
+            HIPCHK(hipMemsetAsync(h->scan_ctr, 0, sizeof(unsigned), h->stream));
+            d.scan_ctr = (unsigned *)h->scan_ctr;
+            h->scan_deferred = false;
+        }
         if (nt == 128)
             hipLaunchKernelGGL((k_qp_ipm<T, R, 128>), dim3(B), dim3(128), lds, h->stream, d, only_active,
                                h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), eta,
@@ -422,6 +431,7 @@ int cmpc_create(cmpc_handle *out, int device, int robot, int N, int max_batch, i
         HIPCHK(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, prio_low));
         HIPCHK(hipEventCreateWithFlags(&h->ev_asm, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&h->ev_scan, hipEventDisableTiming));
+        h->scan_ctr = h->dalloc(16);
         HIPCHK(hipDeviceGetAttribute(&h->n_cu, hipDeviceAttributeMultiprocessorCount, device));
         for (auto &e : h->ev) HIPCHK(hipEventCreate(&e));
         const size_t Bm = max_batch, K1 = N + 1, NB = N + 2, e = h->esz(), NC = h->NC;

@@ -94,6 +94,7 @@ template <typename T> struct DevBuf {
     // SCP
     ScpState *scp;
     unsigned long long *stamps;     // (B,16) per-phase cycle counters (diagnostic builds only)
+    unsigned *scan_ctr;             // k_qp_ipm: covariance-scan job counter (nullptr: no scans)
     T *Xacc, *Uacc, *Kacc, *Sacc;   // accepted solution (B,N+1,9) (B,N,NU) (108,LS) (B,N+1,81)
 };
 

@@ -37,6 +37,7 @@ struct cmpc_handle_s {
     hipStream_t side = nullptr;
     hipEvent_t ev_asm = nullptr, ev_scan = nullptr;
     bool scan_deferred = false, scan_pending = false;
+    void *scan_ctr = nullptr;   // job counter of the scans run by the QP kernel's workgroups
     hipEvent_t ev[5] = {};
     bool timed = false;
     // accumulated timing: one 5-event record per cmpc_scp_iterate since cmpc_timing_reset
@@ -113,6 +114,7 @@ struct cmpc_handle_s {
         d.ws = (T *)ws; d.ws_stride = ws_stride; d.scp = (cmpc::ScpState *)scp;
         d.Xacc = (T *)Xacc; d.Uacc = (T *)Uacc; d.Kacc = (T *)Kacc; d.Sacc = (T *)Sacc;
         d.stamps = (unsigned long long *)stamps;
+        d.scan_ctr = nullptr;
         return d;
     }
 };

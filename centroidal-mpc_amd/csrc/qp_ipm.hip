@@ -21,6 +21,7 @@
 // contiguous 512-B transaction; per-block vectors (nu, r_e) use the same scheme over the N + 2
 // Schur blocks.  The Schur right-hand side / direction dnu never leave LDS.
 #include "common.hpp"
+#include "cov_scan.hpp"
 
 #ifdef CMPC_NOINLINE
 #define PHASE_ATTR __attribute__((noinline))
@@ -2184,6 +2185,25 @@ __global__ void __launch_bounds__(NTT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int o
         for (int i = 0; i < 9; ++i) d.stamps[(size_t)b * 16 + i] = t_acc[i];   // 9..11: k_linearize, 12..15: tw_factor_ends
 #endif
     }
+    // Covariance scans of a deterministic batch (cmpc_api.cpp launch_phase): a workgroup whose QP
+    // has finished takes scan jobs from the counter until none is left, so the scans fill the
+    // SIMDs of problems that converged early.  Every workgroup leaves after one failed take.  Only
+    // the one-wave kernel has the loop (two-wave batches run the scan on a side stream, and the
+    // loop's code costs the two-wave kernel registers).
+    if constexpr (NTT == 64) if (d.scan_ctr) {
+        __shared__ int job;
+        __syncthreads();   // the dynamic LDS is free from here on
+        LdsT<T> *scan_lds = (LdsT<T> *)reinterpret_cast<T *>(dsmem);
+        for (;;) {
+            if (tid == 0) job = (int)atomicAdd(d.scan_ctr, 1u);
+            __syncthreads();
+            const int j = job;
+            __syncthreads();
+            if (j >= d.B) break;
+            if (only_active && !d.scp[j].active) continue;
+            if (tid < 64) cov_scan_problem<T, ROBOT>(d, j, scan_lds);
+        }
+    }
 #undef STAMP
 }
 
@@ -2198,7 +2218,8 @@ INST(float, 1)
 
 size_t ipm_lds_bytes(int N, int prec_bytes, int nt) {
     const size_t vec = (((size_t)(N + 2) * 9 + 7) & ~size_t(7));
-    return (vec + (size_t)2 * SWEEP_LDS + (nt > 64 ? vec : 0)) * prec_bytes;   // + the w_x side array
+    // + the w_x side array; at least one covariance scan's buffers (the scan jobs after the QP)
+    return std::max<size_t>(vec + (size_t)2 * SWEEP_LDS + (nt > 64 ? vec : 0), SCAN_LDS) * prec_bytes;
 }
 
 size_t ipm_workspace_elems(int N, int robot) {

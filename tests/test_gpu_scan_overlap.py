@@ -1,13 +1,15 @@
-"""GPU: the covariance scan beside the QP (cmpc_api.cpp launch_phase, scan_beside_qp).
+"""GPU: the covariance scan off the critical path (cmpc_api.cpp launch_phase).
 
 Inside cmpc_scp_iterate a deterministic batch whose QP leaves SIMDs free (two-wave workgroups, or
-fewer QP waves than SIMDs) runs k_cov_scan on a low-priority side stream, joined behind the QP.
-The phase-by-phase entry points (cmpc_linearize, cmpc_assemble, cmpc_qp_solve, cmpc_accept) keep
-the scan in order on the main stream.  Both orders must give bit-identical X, U, K and Sigma: the
-scan reads only what k_lin_knots wrote and nothing else in the step reads Sigma.  Cases: two-wave
-batch at the metric horizon (overlapped), a small one-wave batch (overlapped), the metric-size
-batch (one wave per SIMD: no overlap) and a stochastic batch (Sigma feeds the assembly: no
-overlap).
+fewer QP waves than SIMDs) runs k_cov_scan on a low-priority side stream, joined behind the QP;
+when the QP fills the device with one wave per SIMD, the QP kernel's workgroups run the scans
+from a job counter once their own problem has converged (k_qp_ipm, cov_scan.hpp).  The
+phase-by-phase entry points (cmpc_linearize, cmpc_assemble, cmpc_qp_solve, cmpc_accept) keep the
+scan kernel in order on the main stream.  All orders must give bit-identical X, U, K and Sigma:
+the scan reads only what k_lin_knots wrote, runs the same code on every path, and nothing else in
+the step reads Sigma.  Cases: two-wave batch at the metric horizon (side stream), a small
+one-wave batch (side stream), the metric-size batch (scans inside the QP kernel) and a
+stochastic batch (Sigma feeds the assembly: in order).
 """
 import numpy as np
 import pytest
