@@ -24,7 +24,10 @@
  * buffers are C-contiguous float64 (int8/int32 where stated) and owned by the caller;
  * the library copies in/out.  Device state is owned by the handle.  A handle is bound to
  * one device and is not thread-safe.  Calls that launch GPU work are asynchronous on the
- * handle's stream unless documented as synchronous; getters synchronize.
+ * handle's stream unless documented as synchronous; getters synchronize.  (Inside
+ * cmpc_scp_iterate the covariance scan of a deterministic batch may run on a second,
+ * low-priority stream of the handle; the handle's stream waits for it behind the QP, so
+ * work ordered after the call on the handle's stream sees its results.)
  *
  * Layouts (B problems, horizon N, nc contacts, nu = 12 controls):
  *   logic (B,N,nc) int8 | pos (B,N,nc,3) | rot (B,N,nc,3,3) | Xbar (B,N+1,9) | Ubar (B,N,nu)
