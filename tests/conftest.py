@@ -9,6 +9,10 @@ for p in (ROOT, os.path.join(ROOT, 'centroidal-mpc_amd')):
         sys.path.insert(0, p)
 
 GOLDEN = os.path.join(ROOT, 'tests', 'golden')
+# tests/golden/make_golden.py FIXTURES: N=20 per robot / gait, BASELINE C1 (trot N=50), the metric
+# horizon (trot N=100), C3's bound N=100, and float32 runs at the reference's own precision
+GOLDEN_TAGS = ('trot', 'trot_stoch', 'bound', 'pace', 'talos', 'trot_n50', 'trot_n100', 'bound_n100',
+               'trot_f32', 'bound_n100_f32')
 
 
 def pytest_configure(config):
@@ -20,7 +24,7 @@ def pytest_configure(config):
 def golden():
     import numpy as np
     out = {}
-    for tag in ('trot', 'trot_stoch', 'bound', 'pace', 'talos'):
+    for tag in GOLDEN_TAGS:
         path = os.path.join(GOLDEN, 'golden_%s.npz' % tag)
         if os.path.exists(path):
             out[tag] = dict(np.load(path, allow_pickle=False))

@@ -9,9 +9,18 @@ uses -- jit = identity, lax.fori_loop = Python loop, dynamic_update_slice, ``.at
 JAX's clamped out-of-range gather, and jacfwd/jacrev by unit forward differences (exact here:
 the centroidal dynamics are linear in each argument separately).  All arithmetic that produces
 the fixtures is the reference's own (src/centroidal_model.py, src/cost.py, src/constraints.py,
-src/scp_solver.py, src/contact_plan.py).  Caveat: the stand-ins compute in float64, the real
-reference (JAX default) in float32.  The osqp stand-in is the oracle's OSQP restatement, so the
-solve_scp fixture pins the state machine around the QP, not the QP solver.
+src/scp_solver.py, src/contact_plan.py).
+
+Precision: the real reference runs its JAX parts in float32 (JAX's default; no x64 flag anywhere in
+the reference).  The fixtures named ``*_f32`` keep that: under them every stand-in array op
+returns float32, as jax.numpy does, and jacfwd returns the exact derivative rounded to float32
+(the differences are taken in float64; the dynamics are affine in each argument, so the difference
+is the derivative).  The other fixtures run the same code in float64.
+
+QP: the osqp stand-in is the oracle's OSQP restatement (ADMM + polish) for the N=20 Solo12
+fixtures, and the oracle's sparse interior-point solver for TALOS (ADMM needs > 20000 iterations
+on its subproblems) and the N >= 50 fixtures.  Either way the solve_scp fixture pins the state
+machine around the QP, not the QP solver (OSQP itself is not installed: parity with it is unpinned).
 
 Only arrays are written (tests/golden/*.npz); no reference source is copied.
 """
@@ -83,26 +92,47 @@ class _At:
         return _U()
 
 
+FP32 = [False]   # set while an *_f32 fixture is generated
+
+
+def _fdt():
+    return np.float32 if FP32[0] else np.float64
+
+
 def _w(x):
-    return np.asarray(x, dtype=float if np.asarray(x).dtype.kind in 'fc' else None).view(JArr) \
-        if not np.isscalar(x) else x
+    if np.isscalar(x):
+        return x
+    a = np.asarray(x)
+    return np.asarray(a, dtype=_fdt() if a.dtype.kind in 'fc' else None).view(JArr)
 
 
 def _jacfwd(f, argnums=0):
     def jf(*args):
-        args = list(args)
-        x0 = np.asarray(args[argnums], float)
-        f0 = np.asarray(f(*args), float)
-        J = np.zeros(f0.shape + x0.shape)
-        for i in np.ndindex(*x0.shape):
-            xp = x0.copy(); xp[i] += 1.0
-            a2 = list(args); a2[argnums] = xp.view(JArr)
-            J[(Ellipsis,) + i] = np.asarray(f(*a2), float) - f0
-        return J.view(JArr)
+        # differences in float64 even for the float32 fixtures: the result is the exact
+        # derivative (affine dynamics), rounded once to the working precision as forward-mode
+        # AD in float32 would be
+        was = FP32[0]
+        FP32[0] = False
+        try:
+            args = [np.asarray(a, float).view(JArr) if isinstance(a, np.ndarray) and a.dtype.kind == 'f' else a
+                    for a in args]
+            x0 = np.asarray(args[argnums], float)
+            f0 = np.asarray(f(*args), float)
+            J = np.zeros(f0.shape + x0.shape)
+            for i in np.ndindex(*x0.shape):
+                xp = x0.copy(); xp[i] += 1.0
+                a2 = list(args); a2[argnums] = xp.view(JArr)
+                J[(Ellipsis,) + i] = np.asarray(f(*a2), float) - f0
+        finally:
+            FP32[0] = was
+        return _w(J)
     return jf
 
 
-def install_standins(qp_solver):
+QP = [None]   # the osqp stand-in's solver for the fixture being generated
+
+
+def install_standins():
     jax = types.ModuleType('jax')
     jnp = types.ModuleType('jax.numpy')
     for name in ('zeros', 'ones', 'eye', 'hstack', 'vstack', 'cross', 'arange', 'where', 'einsum', 'sum',
@@ -110,10 +140,13 @@ def install_standins(qp_solver):
         fn = getattr(np, name)
         setattr(jnp, name, (lambda fn_: lambda *a, **k: _w(fn_(*a, **k)))(fn))
     jnp.array = lambda x, *a, **k: _w(np.array(x, *a, **k))
+    jnp.float32 = np.float32
     jnp.array_split = lambda x, n, *a: [_w(v) for v in np.array_split(np.asarray(x), n, *a)]
     jnp.linalg = types.SimpleNamespace(solve=lambda A, b: _w(np.linalg.solve(A, b)))
 
     def _to_j(a):
+        if isinstance(a, np.ndarray) and a.dtype.kind == 'f' and a.dtype != _fdt():
+            return np.asarray(a, _fdt()).view(JArr)   # a device array holds JAX's default float
         if isinstance(a, np.ndarray) and not isinstance(a, JArr):
             return a.view(JArr)
         if isinstance(a, dict):
@@ -187,7 +220,7 @@ def install_standins(qp_solver):
             self.args = (P, q, A, l, u)
 
         def solve(self):
-            return qp_solver(*self.args)
+            return QP[0](*self.args)
     osqp.OSQP = OSQP
     sys.modules['osqp'] = osqp
 
@@ -213,7 +246,16 @@ def make_conf(kind, N):
     return conf, rob
 
 
-def generate(kind, N, stochastic, tag, out):
+def generate(kind, N, stochastic, tag, out, qp, fp32=False):
+    QP[0] = qp
+    FP32[0] = fp32
+    try:
+        _generate(kind, N, stochastic, tag, out, fp32)
+    finally:
+        FP32[0] = False
+
+
+def _generate(kind, N, stochastic, tag, out, fp32):
     from src.contact_plan import create_contact_sequence as ref_seq   # reference module
     conf, rob = make_conf(kind, N)
     gait = dict(conf.gait)
@@ -260,7 +302,7 @@ def generate(kind, N, stochastic, tag, out):
             sol = scp.solve_scp(model, conf.scp_params)
         finally:
             os.chdir(cwd)
-    d = dict(kind=kind, N=N, stochastic=int(stochastic), Xnpz=X,
+    d = dict(kind=kind, N=N, stochastic=int(stochastic), fp32=int(fp32), Xnpz=X,
              logic=np.asarray(model._contact_data['contacts_logic']),
              pos=np.asarray(model._contact_data['contacts_position']),
              rot=np.asarray(model._contact_data['contacts_orient']),
@@ -288,6 +330,17 @@ def generate(kind, N, stochastic, tag, out):
     print('wrote', tag, 'scp_ok', d['scp_ok'])
 
 
+def FIXTURES(admm, ipm):
+    """(kind, N, stochastic, tag, QP stand-in, float32).  N=50 is BASELINE C1's horizon, N=100
+    the metric config's and C2 / C3's; bound_n100_f32 is C3 at the reference's own precision."""
+    return (('trot', 20, False, 'trot', admm, False), ('trot', 20, True, 'trot_stoch', admm, False),
+            ('bound', 20, False, 'bound', admm, False), ('pace', 20, False, 'pace', admm, False),
+            ('talos', 20, False, 'talos', ipm, False),
+            ('trot', 50, False, 'trot_n50', ipm, False), ('trot', 100, False, 'trot_n100', ipm, False),
+            ('bound', 100, False, 'bound_n100', ipm, False),
+            ('trot', 20, False, 'trot_f32', ipm, True), ('bound', 100, False, 'bound_n100_f32', ipm, True))
+
+
 def main():
     if not os.path.isdir(REF):
         print('reference not present; nothing to do')
@@ -297,19 +350,22 @@ def main():
     from cmpc import synth
     from config import _robots
     from oracle.osqp_admm import solve_qp as oracle_qp
+    from oracle.sparse_ipm import solve_qp as sparse_ipm_qp
     PRODUCT.update(confs={k: synth.load_conf(k) for k in ('trot', 'bound', 'pace', 'talos')},
                    warm_start=synth.warm_start, solo_feet=_robots.SOLO12_FEET, talos_feet=_robots.TALOS_FEET)
     # 2. swap in the reference's src/ package under the stand-ins
     for m in [m for m in sys.modules if m in ('src', 'config') or m.startswith(('src.', 'config.'))]:
         del sys.modules[m]
-    install_standins(lambda P, q, A, l, u: oracle_qp(P, q, A, l, u, max_iter=20000))
+    install_standins()
     sys.path.insert(0, REF)
     import src  # noqa: F401
     assert os.path.realpath(os.path.dirname(src.__file__)).startswith(os.path.realpath(REF)), src.__file__
-    for kind, N, stoch, tag in (('trot', 20, False, 'trot'), ('trot', 20, True, 'trot_stoch'),
-                                ('bound', 20, False, 'bound'), ('pace', 20, False, 'pace'),
-                                ('talos', 20, False, 'talos')):
-        generate(kind, N, stoch, tag, HERE)
+    admm = lambda P, q, A, l, u: oracle_qp(P, q, A, l, u, max_iter=20000)
+    ipm = lambda P, q, A, l, u: sparse_ipm_qp(P, q, A, l, u)
+    want = sys.argv[1:]
+    for kind, N, stoch, tag, qp, f32 in FIXTURES(admm, ipm):
+        if not want or tag in want:
+            generate(kind, N, stoch, tag, HERE, qp, f32)
 
 
 if __name__ == '__main__':

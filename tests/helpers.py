@@ -5,7 +5,24 @@ from scipy import sparse
 from cmpc.problem import ModelParams, ProblemBatch
 from cmpc.synth import load_conf
 
-KIND_CONF = {'trot': 'trot', 'trot_stoch': 'trot', 'bound': 'bound', 'pace': 'pace', 'talos': 'talos'}
+KIND_CONF = {'trot': 'trot', 'trot_stoch': 'trot', 'bound': 'bound', 'pace': 'pace', 'talos': 'talos',
+             'trot_n50': 'trot', 'trot_n100': 'trot', 'bound_n100': 'bound', 'trot_f32': 'trot',
+             'bound_n100_f32': 'bound'}
+
+
+def golden_fp32(g):
+    """True for the fixtures made at the reference's own float32 precision (``*_f32``)."""
+    return bool(int(g['fp32'])) if 'fp32' in g else False
+
+
+def golden_qp(tag, g):
+    """The QP stand-in the fixture's solve_scp ran with (tests/golden/make_golden.py FIXTURES):
+    the OSQP restatement for the N=20 Solo12 fixtures, the sparse IPM for the others."""
+    from oracle.osqp_admm import solve_qp
+    from oracle.sparse_ipm import solve_qp as sparse_ipm
+    if tag in ('trot', 'trot_stoch', 'bound', 'pace'):
+        return lambda *a: solve_qp(*a, max_iter=20000)
+    return sparse_ipm
 
 
 def golden_params(tag, g):

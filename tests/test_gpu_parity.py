@@ -242,21 +242,23 @@ def test_qp_horizon_edges(cfg, N, B):
 
 
 @pytest.mark.parametrize('cfg,N,B,prec,mixed', [
+    ('trot', 100, 256, 'fp64', None),            # BASELINE C2: two waves per problem, one end of the
+                                                 # Schur recurrence per wave (tw_factor_ends<T, 64>)
     ('bound', 100, 1024, 'fp32', None),          # BASELINE C3: fp32 + tolerance check vs CPU
     ('talos', 200, 512, 'fp64', None),           # BASELINE C4: one GPU's shard of 4096
     ('trot', 150, 1024, 'fp64', ('pace', 'trot')),  # BASELINE C5: one GPU's shard of 8192, mixed plans
 ])
 def test_full_size_baseline_configs(cfg, N, B, prec, mixed):
-    """Full per-GPU sizes of BASELINE C3-C5: every QP solved; on a sample, KKT primal residual of
-    the reference-form QP (fp64 1e-8, fp32 1e-3) and |X| within 1e-5 (fp64) / 5e-3 (fp32) of the
-    oracle's independent sparse IPM on the same QP."""
+    """Full per-GPU sizes of BASELINE C2-C5: every QP solved; on a sample (first, middle, last
+    problem), KKT primal residual of the reference-form QP (fp64 1e-8, fp32 1e-3) and |X| within
+    1e-5 (fp64) / 5e-3 (fp32) of the oracle's independent sparse IPM on the same QP."""
     pb, s = _solver(cfg, N, B, prec, mixed=mixed)
     s.scp_iterate(fixed_iters=True)
     z, y, st, it = s.qp_solution(with_y=True)
     assert np.all(st == 1), np.unique(st, return_counts=True)
     nx = 9 * (N + 1)
     tol_prim, tol_x = (1e-3, 5e-3) if prec == 'fp32' else (1e-8, 1e-5)
-    for b in (0, B - 1):
+    for b in (0, B // 2 + 1, B - 1):
         P, q, A, l, u = s.export_qp(b)
         k = kkt_residuals(P, q, A, l, u, z[b])
         assert k['prim'] <= tol_prim, (b, k)
@@ -267,14 +269,16 @@ def test_full_size_baseline_configs(cfg, N, B, prec, mixed):
 
 
 def test_talos_shrunk_trust_region_qp_solves():
-    """BASELINE C4 shard (TALOS N=200 x 512), second fixed-K SCP iteration (weight raised to 500 by
-    the first iteration's trust-region rejects): every QP reaches 'solved' with merit <= 1.  Round 1
+    """BASELINE C4 shard (TALOS N=200 x 512) with the trust region of round 1's second fixed-K SCP
+    iteration (weight 500 after a trust-region reject at radius 100; since radius0 = 1000 the
+    first iteration accepts, so the weight is set directly): every QP reaches 'solved' with merit
+    <= 1.  Round 1
     stalled on problem 280 here (60 iterations, status -2); iterative refinement of the corrector
     direction fixes it (tests/test_ipm_mirror.py reproduces the stall and the fix on the CPU).
     The slowest problem matches the oracle's sparse IPM on the same exported QP."""
     N, B = 200, 512
     pb, s = _solver('talos', N, B)
-    s.scp_iterate(fixed_iters=True)
+    s.set_trust_region(weight=500.0, radius=100.0)
     s.scp_iterate(fixed_iters=True)
     z, y, st, it = s.qp_solution(with_y=True)
     merit, nref = s.qp_info()
