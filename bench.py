@@ -44,7 +44,7 @@ METRIC = 'SCP iterations/sec, Solo12-trot N=100 batch=1024 @ 1/2/4/8 GPU'
 WORKLOAD_NAMES = {'trot': 'conf_solo12_trot', 'bound': 'conf_solo12_bound', 'pace': 'conf_solo12_pace',
                   'talos': 'conf_talos', 'mixed': 'Solo12 pace+trot mixed contact plans'}
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
-CPU_SHARE = 16          # host cores of one GPU's share on the box
+CPU_WORKERS_CAP = 128   # memory bound on forked oracle workers (~0.2 GB each)
 
 
 def per_knot_sizes(robot):
@@ -88,20 +88,58 @@ def cpu_info():
         affinity = len(os.sched_getaffinity(0))
     except AttributeError:
         affinity = os.cpu_count()
-    return dict(os_cpu_count=os.cpu_count(), affinity=affinity, model=model)
+    quota, source = cpu_quota()
+    return dict(os_cpu_count=os.cpu_count(), affinity=affinity, model=model, cgroup_quota=quota,
+                quota_source=source)
+
+
+def cpu_quota():
+    """CPUs this process may use by its cgroup's CFS quota: (quota in CPUs or None, source).
+    cgroup v2 ``cpu.max`` ("<quota> <period>" or "max <period>"), else cgroup v1
+    ``cpu.cfs_quota_us`` / ``cpu.cfs_period_us``; None when unlimited or unreadable."""
+    try:
+        for line in open('/proc/self/cgroup'):
+            parts = line.strip().split(':', 2)
+            if len(parts) == 3 and parts[0] == '0':            # v2 unified hierarchy
+                path = os.path.join('/sys/fs/cgroup', parts[2].lstrip('/'), 'cpu.max')
+                for p in (path, '/sys/fs/cgroup/cpu.max'):
+                    if os.path.exists(p):
+                        q, per = open(p).read().split()[:2]
+                        if q == 'max':
+                            return None, p + ' (max)'
+                        return float(q) / float(per), p
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open('/sys/fs/cgroup/cpu/cpu.cfs_quota_us').read())
+        per = int(open('/sys/fs/cgroup/cpu/cpu.cfs_period_us').read())
+        if q > 0:
+            return q / per, '/sys/fs/cgroup/cpu/cpu.cfs_quota_us'
+        return None, '/sys/fs/cgroup/cpu/cpu.cfs_quota_us (unlimited)'
+    except (OSError, ValueError):
+        return None, 'no cgroup cpu limit found'
+
+
+def cpu_workers(info):
+    """min(affinity, cgroup quota) worker processes (all the CPUs the host gives
+    this process), capped at CPU_WORKERS_CAP for memory."""
+    n = info['affinity'] or os.cpu_count() or 1
+    if info['cgroup_quota']:
+        n = min(n, max(1, int(info['cgroup_quota'])))
+    return max(1, min(n, CPU_WORKERS_CAP))
 
 
 def cpu_baseline(N):
     """The oracle on the GPU box's host cores, bounded samples (~15-25 s in all):
-    throughput: 96 problems per worker x one SCP iteration, over the box's CPU share (16 workers;
-      os.cpu_count() reports the whole machine there, see cpu_info);
+    throughput: 96 problems per worker x one SCP iteration, min(affinity, cgroup CPU quota) worker
+      processes (cpu_workers; os.cpu_count() reports the whole machine there, see cpu_info);
     latency: one core, 6 problems x one SCP iteration (seconds per problem iteration);
     early exit: the reference's loop (src/scp_solver.py:118-179, exits after the first accept) on
       8 problems per worker."""
     import multiprocessing as mp
     from cmpc.synth import make_batch
     info = cpu_info()
-    cores = max(1, min(CPU_SHARE, info['affinity'] or 1))
+    cores = cpu_workers(info)
     n_prob = 96 * cores
     pb = make_batch('trot', N, n_prob, seed_offset=777)
     probs = [pb.oracle_problem(b) for b in range(n_prob)]
@@ -123,7 +161,9 @@ def cpu_baseline(N):
     return dict(value=n_prob / dt, unit='SCP iterations/s', cores=cores, kind='port',
                 sample='%d synthetic Solo12-trot N=%d problems, one SCP iteration each (oracle: numpy '
                        'linearization + reference-order CSC assembly + OSQP-algorithm ADMM eps 1e-7 with '
-                       'polish), %d worker processes, %.1f s wall' % (n_prob, N, cores, dt),
+                       'polish), %d worker processes (min of affinity %s and cgroup quota %s from %s, cap %d), %.1f s wall'
+                       % (n_prob, N, cores, info['affinity'], info['cgroup_quota'], info['quota_source'],
+                          CPU_WORKERS_CAP, dt),
                 host=info,
                 single_core_latency_s=lat,
                 early_exit=dict(value=sum(iters) / dt_ee, unit='SCP iterations/s', problems=len(ee),

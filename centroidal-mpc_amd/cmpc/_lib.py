@@ -56,6 +56,17 @@ class Timing(ctypes.Structure):
                 ('accept_ms', ctypes.c_float), ('total_ms', ctypes.c_float)]
 
 
+class IterRecord(ctypes.Structure):
+    """include/cmpc.h cmpc_iter_record"""
+    _fields_ = [('weight', ctypes.c_double), ('radius', ctypes.c_double), ('tr_norm', ctypes.c_double),
+                ('rho', ctypes.c_double), ('iteration', ctypes.c_int32), ('qp_status', ctypes.c_int32),
+                ('qp_iters', ctypes.c_int32), ('decision', ctypes.c_int32)]
+
+
+ITER_RECORD_DTYPE = np.dtype([('weight', 'f8'), ('radius', 'f8'), ('tr_norm', 'f8'), ('rho', 'f8'),
+                              ('iteration', 'i4'), ('qp_status', 'i4'), ('qp_iters', 'i4'), ('decision', 'i4')])
+DECISIONS = {1: 'accept', 2: 'reject_rho', 3: 'reject_tr', -1: 'qp_failed'}
+
 EXPORTS = ['cmpc_create', 'cmpc_destroy', 'cmpc_last_error', 'cmpc_version', 'cmpc_default_qp_settings',
            'cmpc_set_qp_settings', 'cmpc_set_params', 'cmpc_upload', 'cmpc_set_trust_region', 'cmpc_rollout',
            'cmpc_linearize', 'cmpc_assemble',
@@ -66,7 +77,8 @@ EXPORTS = ['cmpc_create', 'cmpc_destroy', 'cmpc_last_error', 'cmpc_version', 'cm
            'cmpc_get_linearization_point', 'cmpc_interpolate', 'cmpc_generate_contact_plans',
            'cmpc_upload_states', 'cmpc_get_contact_plans', 'cmpc_get_warm_start', 'cmpc_get_qp_info',
            'cmpc_comm_get_unique_id', 'cmpc_comm_init', 'cmpc_comm_destroy', 'cmpc_comm_bcast_params',
-           'cmpc_comm_allreduce_max', 'cmpc_comm_gather_solution', 'cmpc_load_qp']
+           'cmpc_comm_allreduce_max', 'cmpc_comm_gather_solution', 'cmpc_load_qp', 'cmpc_get_iteration_history',
+           'cmpc_get_accepted']
 SCP_MODE = {'reference': 0, 'gusto': 1}
 
 _lib = None
@@ -129,6 +141,8 @@ def load():
         'cmpc_comm_allreduce_max': (i32, [h, vp, i32]),
         'cmpc_comm_gather_solution': (i32, [h, i32, vp, vp, vp, vp, vp]),
         'cmpc_load_qp': (i32, [h, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+        'cmpc_get_iteration_history': (i32, [h, i32, vp, vp]),
+        'cmpc_get_accepted': (i32, [h, i32, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -183,9 +197,12 @@ class Solver:
         self.prec = PREC[precision]
         self.max_batch = int(max_batch)
         self.B = 0
+        self._params = []
         self._epoch = 0   # counts C-ABI calls: a cached export is valid only while no call followed it
         h = ctypes.c_void_p()
         rc = self.lib.cmpc_create(ctypes.byref(h), int(device), ROBOTS[robot], self.N, self.max_batch, self.prec)
+        if rc == -5:
+            raise CmpcError('cmpc_create: TALOS handles need fp64 (its QPs do not converge in fp32)')
         if rc != 0 or not h.value:
             raise CmpcError('cmpc_create failed (rc=%d): no usable GPU / HIP runtime?' % rc)
         self.h = h
@@ -228,6 +245,7 @@ class Solver:
         self._chk(self.lib.cmpc_set_qp_settings(self.h, ctypes.byref(s)), 'cmpc_set_qp_settings')
 
     def set_params(self, params):
+        self._params = list(params)
         arr = (Params * len(params))(*[params_struct(p, self.nc) for p in params])
         self._chk(self.lib.cmpc_set_params(self.h, len(params), arr), 'cmpc_set_params')
 
@@ -411,6 +429,29 @@ class Solver:
         keys = ('tr_norm', 'rho', 'qp_status', 'qp_iters', 'decision')
         self._chk(self.lib.cmpc_get_iteration_log(self.h, *[_ptr(out[k]) for k in keys]), 'cmpc_get_iteration_log')
         return out
+
+    def iteration_history(self, cap=None):
+        """Every SCP iteration of every problem since the upload (cmpc_get_iteration_history):
+        (records (B, cap) of ITER_RECORD_DTYPE, n_records (B)); cap defaults to the largest
+        max_iterations of the uploaded parameter classes."""
+        if cap is None:
+            cap = max(int(p.scp_params.get('max_iterations', 10)) for p in self._params) if self._params else 10
+        rec = np.zeros((self.B, int(cap)), ITER_RECORD_DTYPE)
+        n = np.zeros(self.B, np.int32)
+        assert ITER_RECORD_DTYPE.itemsize == ctypes.sizeof(IterRecord)
+        self._chk(self.lib.cmpc_get_iteration_history(self.h, int(cap), _ptr(rec), _ptr(n)),
+                  'cmpc_get_iteration_history')
+        return rec, n
+
+    def accepted(self, j, with_ks=True):
+        """Accepted iterate j of every problem (cmpc_get_accepted): X (B,N+1,9), U (B,N,12) and, with
+        with_ks, K (B,N,12,9), Sigma (B,N+1,9,9); zeros for problems with fewer accepts."""
+        B, N = self.B, self.N
+        X = np.zeros((B, N + 1, 9)); U = np.zeros((B, N, 12))
+        K = np.zeros((B, N, 12, 9)) if with_ks else None
+        S = np.zeros((B, N + 1, 9, 9)) if with_ks else None
+        self._chk(self.lib.cmpc_get_accepted(self.h, int(j), _ptr(X), _ptr(U), _ptr(K), _ptr(S)), 'cmpc_get_accepted')
+        return dict(X=X, U=U, K=K, Sigma=S)
 
     def timing(self):
         t = Timing()

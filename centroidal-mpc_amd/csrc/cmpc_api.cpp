@@ -176,8 +176,10 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
             h->lin_dense = true;
         }
         h->lin_lane_done = h->lin_lane;
-        if (overlap && !any_stochastic(h))
+        if (overlap && !any_stochastic(h)) {
             h->scan_deferred = true;   // beside the QP (case 1) or inside it (case 2)
+            h->scan_oa = only_active;
+        }
         else
             launch_scan<T, R>(h, h->stream, only_active);
         break;
@@ -313,7 +315,12 @@ template <typename T, int R> void ensure_dense_impl(cmpc_handle h) {
     hipLaunchKernelGGL((k_lin_knots<T, R>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream, d, 0, 1);
     HIPCHK(hipGetLastError());
 }
+}  // namespace
+
+namespace cmpc_host {
+
 void ensure_dense(cmpc_handle h) {
+    settle_all(h);
     if (h->lin_dense || !h->lin_lane_done || h->B == 0) return;
     if (h->prec == CMPC_PREC_F64) {
         if (h->robot == 0) ensure_dense_impl<double, 0>(h); else ensure_dense_impl<double, 1>(h);
@@ -322,6 +329,39 @@ void ensure_dense(cmpc_handle h) {
     }
     h->lin_dense = true;
 }
+
+
+// Reference mode serves accepted K / Sigma from the live arrays (cmpc_handle_::ks_live); before
+// anything can make them differ from the accepted iteration's (GuSTO mode moves the linearization
+// point, new contact plans change it), they are copied to Kacc / Sacc once and copied per accept
+// from then on.
+void materialize_accepted_ks(cmpc_handle h) {
+    if (!h->ks_live) return;
+    settle_all(h);   // Sigma of a deferred scan first
+    if (h->B > 0) {
+        const size_t e = h->esz();
+        HIPCHK(hipMemcpyAsync(h->Kacc, h->K, (size_t)h->max_batch * h->N * NU * 9 * e, hipMemcpyDeviceToDevice, h->stream));
+        HIPCHK(hipMemcpyAsync(h->Sacc, h->Sig, (size_t)h->max_batch * (h->N + 1) * 81 * e, hipMemcpyDeviceToDevice, h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+    }
+    h->ks_live = false;
+}
+
+
+// A scan left deferred or running on the side stream (cmpc_scp_iterate stopped between its phases,
+// e.g. by an error) is settled before anything reads Sigma or relaunches the linearization.
+void settle_all(cmpc_handle h) {
+    if (!h->scan_deferred && !h->scan_pending) return;
+    if (h->prec == CMPC_PREC_F64) {
+        if (h->robot == 0) settle_scan<double, 0>(h, h->scan_oa); else settle_scan<double, 1>(h, h->scan_oa);
+    } else {
+        if (h->robot == 0) settle_scan<float, 0>(h, h->scan_oa); else settle_scan<float, 1>(h, h->scan_oa);
+    }
+}
+
+}  // namespace cmpc_host
+
+namespace {
 
 void phase(cmpc_handle h, int ph, int only_active, bool overlap = false) {
     need(h->B > 0, "no problems uploaded");
@@ -335,7 +375,33 @@ void phase(cmpc_handle h, int ph, int only_active, bool overlap = false) {
     }
 }
 
+// Iteration records and accepted-iterate slots for max(max_iterations) iterations per problem (the
+// reference appends every accepted iterate, src/scp_solver.py:162-167); the K / Sigma slots only
+// in GuSTO mode, where they differ between accepts.  Grown before an iteration needs them; a
+// regrow drops earlier records (capacity changes only with new parameter classes).
+void ensure_history(cmpc_handle h) {
+    int cap = 1;
+    for (auto &p : h->hparams) cap = std::max(cap, (int)p.max_iterations);
+    cap = std::min(cap, 4096);
+    const size_t Bm = h->max_batch, K1 = h->N + 1, e = h->esz(), LS = (size_t)h->max_batch * h->N;
+    if (h->log_cap < cap) {
+        h->regrow(h->hlog, Bm * cap * sizeof(cmpc_iter_record));
+        h->log_cap = cap;
+    }
+    if (h->hist_cap < cap) {
+        h->regrow(h->hX, (size_t)cap * Bm * K1 * 9 * e);
+        h->regrow(h->hU, (size_t)cap * Bm * h->N * NU * e);
+        h->hist_cap = cap;
+    }
+    if (h->scp_mode == CMPC_SCP_MODE_GUSTO && h->hks_cap < h->hist_cap) {
+        h->regrow(h->hK, (size_t)h->hist_cap * NU * 9 * LS * e);
+        h->regrow(h->hS, (size_t)h->hist_cap * Bm * K1 * 81 * e);
+        h->hks_cap = h->hist_cap;
+    }
+}
+
 void reset_scp(cmpc_handle h, const int32_t *class_id) {
+    settle_all(h);   // a scan still pending reads the previous batch's arrays
     h->ks_live = h->scp_mode == CMPC_SCP_MODE_REFERENCE;
     h->lin_lane_done = false;   // new inputs: nothing to recompute densely until the next linearization
     std::vector<ScpState> st(h->B);
@@ -365,21 +431,6 @@ void dl_knots(cmpc_handle h, double *dst, const void *src, size_t kn0, size_t n,
                            (int)ne, tmp);
     HIPCHK(hipGetLastError());
     from_dev_raw(h, dst, tmp, n * ne * sizeof(double));
-}
-
-// Reference mode serves accepted K / Sigma from the live arrays (cmpc_handle_::ks_live); before
-// anything can make them differ from the accepted iteration's (GuSTO mode moves the linearization
-// point, new contact plans change it), they are copied to Kacc / Sacc once and copied per accept
-// from then on.
-void materialize_accepted_ks(cmpc_handle h) {
-    if (!h->ks_live) return;
-    if (h->B > 0) {
-        const size_t e = h->esz();
-        HIPCHK(hipMemcpyAsync(h->Kacc, h->K, (size_t)h->max_batch * h->N * NU * 9 * e, hipMemcpyDeviceToDevice, h->stream));
-        HIPCHK(hipMemcpyAsync(h->Sacc, h->Sig, (size_t)h->max_batch * (h->N + 1) * 81 * e, hipMemcpyDeviceToDevice, h->stream));
-        HIPCHK(hipStreamSynchronize(h->stream));
-    }
-    h->ks_live = false;
 }
 
 std::vector<ScpState> get_scp(cmpc_handle h) {
@@ -414,6 +465,11 @@ int cmpc_create(cmpc_handle *out, int device, int robot, int N, int max_batch, i
     if (robot != 0 && robot != 1) return -2;
     if (N < 2 || N > 255 || max_batch < 1) return -2;
     if (precision != CMPC_PREC_F64 && precision != CMPC_PREC_F32) return -2;
+    // TALOS QPs need fp64: the CoP rows at centimetre scale next to the friction rows, and
+    // D = lambda / s spanning 1e15 (fp64 needs iterative refinement there), took every
+    // fp32 solve to non-finite values by its third Newton step (N = 40).  Every BASELINE TALOS
+    // configuration is fp64.
+    if (robot == CMPC_ROBOT_TALOS && precision == CMPC_PREC_F32) return -5;
     cmpc_handle h = new cmpc_handle_s();
     h->device = device; h->robot = robot; h->N = N; h->max_batch = max_batch; h->prec = precision;
     h->NC = robot == 0 ? 4 : 2;
@@ -513,6 +569,9 @@ int cmpc_set_qp_settings(cmpc_handle h, const cmpc_qp_settings *s) {
 int cmpc_set_params(cmpc_handle h, int n_classes, const cmpc_params *classes) {
     return guard(h, [&] {
         need(n_classes > 0 && classes, "no parameter classes");
+        // new R or noise change the next linearization's K / Sigma: the accepted ones are copied out
+        // of the live arrays first
+        materialize_accepted_ks(h);
         for (int i = 0; i < n_classes; ++i) {
             const cmpc_params &p = classes[i];
             need(p.mass > 0 && p.dt > 0 && p.mu > 0, "invalid mass/dt/mu");
@@ -719,11 +778,17 @@ int cmpc_rollout(cmpc_handle h, const double *X, const double *U, double *out) {
 int cmpc_linearize(cmpc_handle h) { return guard(h, [&] { phase(h, 0, 0); }); }
 int cmpc_assemble(cmpc_handle h) { return guard(h, [&] { phase(h, 1, 0); }); }
 int cmpc_qp_solve(cmpc_handle h) { return guard(h, [&] { phase(h, 2, 0); }); }
-int cmpc_accept(cmpc_handle h, int fixed_iters) { return guard(h, [&] { phase(h, 3, fixed_iters ? 0 : 1); }); }
+int cmpc_accept(cmpc_handle h, int fixed_iters) {
+    return guard(h, [&] {
+        ensure_history(h);
+        phase(h, 3, fixed_iters ? 0 : 1);
+    });
+}
 
 int cmpc_scp_iterate(cmpc_handle h, int fixed_iters) {
     return guard(h, [&] {
         const int oa = fixed_iters ? 0 : 1;
+        ensure_history(h);
         hipEvent_t *ev = h->ev;
         if (h->accumulate) {
             if (h->ev_used == h->ev_pool.size()) {
@@ -964,6 +1029,7 @@ int cmpc_get_qp_info(cmpc_handle h, double *merit, int32_t *n_refine) {
 int cmpc_get_solution(cmpc_handle h, double *X, double *U, double *K, double *Sigma, int32_t *n_accepted,
                       int32_t *iterations, int32_t *scp_status, double *weight, double *radius) {
     return guard(h, [&] {
+        settle_all(h);
         const size_t B = h->B, N = h->N, K1 = N + 1;
         auto dl = [&](double *dst, void *src, size_t n) {
             if (h->prec == CMPC_PREC_F64) from_dev<double>(h, dst, src, n); else from_dev<float>(h, dst, src, n);
@@ -993,6 +1059,63 @@ int cmpc_get_iteration_log(cmpc_handle h, double *tr_norm, double *rho, int32_t 
             if (qp_status) qp_status[b] = st[b].qp_status;
             if (qp_iters) qp_iters[b] = st[b].qp_iters;
             if (decision) decision[b] = st[b].decision;
+        }
+    });
+}
+
+int cmpc_get_iteration_history(cmpc_handle h, int cap, cmpc_iter_record *records, int32_t *n_records) {
+    return guard(h, [&] {
+        need(h->B > 0, "no problems uploaded");
+        need(cap >= 1, "cap must be >= 1");
+        auto st = get_scp(h);
+        std::vector<cmpc_iter_record> all;
+        if (h->log_cap > 0) {
+            all.resize((size_t)h->B * h->log_cap);
+            from_dev_raw(h, all.data(), h->hlog, all.size() * sizeof(cmpc_iter_record));
+        }
+        for (int b = 0; b < h->B; ++b) {
+            const int n = std::min(std::min(st[b].iter, h->log_cap), cap);
+            if (n_records) n_records[b] = n;
+            if (!records) continue;
+            for (int i = 0; i < cap; ++i) {
+                cmpc_iter_record r{};
+                if (i < n) r = all[(size_t)b * h->log_cap + i];
+                records[(size_t)b * cap + i] = r;
+            }
+        }
+    });
+}
+
+int cmpc_get_accepted(cmpc_handle h, int j, double *X, double *U, double *K, double *Sigma) {
+    return guard(h, [&] {
+        need(h->B > 0, "no problems uploaded");
+        need(j >= 0, "accepted index must be >= 0");
+        settle_all(h);
+        const size_t B = h->B, N = h->N, K1 = N + 1, Bm = h->max_batch, e = h->esz();
+        const size_t LS = Bm * N;
+        auto st = get_scp(h);
+        bool any = false;
+        for (size_t b = 0; b < B; ++b) any |= j < st[b].n_accepted;
+        need(!any || j < h->hist_cap, "accepted iterate beyond the kept history (max_iterations)");
+        auto dl = [&](double *dst, void *src, size_t n) {
+            if (h->prec == CMPC_PREC_F64) from_dev<double>(h, dst, src, n); else from_dev<float>(h, dst, src, n);
+        };
+        if (any) {
+            dl(X, (char *)h->hX + (size_t)j * Bm * K1 * 9 * e, B * K1 * 9);
+            dl(U, (char *)h->hU + (size_t)j * Bm * N * NU * e, B * N * NU);
+            const bool gusto_ks = h->hks_cap > j && !h->ks_live && h->scp_mode == CMPC_SCP_MODE_GUSTO;
+            // reference mode: the accepted K / Sigma are the fixed linearization point's (Q1)
+            dl_knots(h, K, gusto_ks ? (char *)h->hK + (size_t)j * NU * 9 * LS * e : (h->ks_live ? h->K : h->Kacc), 0,
+                     B * N, NU * 9);
+            dl(Sigma, gusto_ks ? (char *)h->hS + (size_t)j * Bm * K1 * 81 * e : (h->ks_live ? h->Sig : h->Sacc),
+               B * K1 * 81);
+        }
+        for (size_t b = 0; b < B; ++b) {
+            if (any && j < st[b].n_accepted) continue;
+            if (X) std::fill(X + b * K1 * 9, X + (b + 1) * K1 * 9, 0.0);
+            if (U) std::fill(U + b * N * NU, U + (b + 1) * N * NU, 0.0);
+            if (K) std::fill(K + b * N * NU * 9, K + (b + 1) * N * NU * 9, 0.0);
+            if (Sigma) std::fill(Sigma + b * K1 * 81, Sigma + (b + 1) * K1 * 81, 0.0);
         }
     });
 }

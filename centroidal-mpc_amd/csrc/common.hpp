@@ -96,6 +96,12 @@ template <typename T> struct DevBuf {
     unsigned long long *stamps;     // (B,16) per-phase cycle counters (diagnostic builds only)
     unsigned *scan_ctr;             // k_qp_ipm: covariance-scan job counter (nullptr: no scans)
     T *Xacc, *Uacc, *Kacc, *Sacc;   // accepted solution (B,N+1,9) (B,N,NU) (108,LS) (B,N+1,81)
+    // per-iteration records (B, log_cap) and accepted-iterate history: slot j of X (B,N+1,9),
+    // U (B,N,NU), K (108,LS) element-major, Sigma (B,N+1,81), hist_cap slots (K, Sigma: GuSTO
+    // mode only; nullptr when not allocated)
+    cmpc_iter_record *hlog;
+    int log_cap, hist_cap;
+    T *hX, *hU, *hK, *hS;
 };
 
 // ---------------------------------------------------------------- knot-minor layouts

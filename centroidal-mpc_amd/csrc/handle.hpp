@@ -37,6 +37,7 @@ struct cmpc_handle_s {
     hipStream_t side = nullptr;
     hipEvent_t ev_asm = nullptr, ev_scan = nullptr;
     bool scan_deferred = false, scan_pending = false;
+    int scan_oa = 0;            // only_active of the deferred scan (settle_all)
     void *scan_ctr = nullptr;   // job counter of the scans run by the QP kernel's workgroups
     hipEvent_t ev[5] = {};
     bool timed = false;
@@ -73,6 +74,10 @@ struct cmpc_handle_s {
     int comm_rank = 0, comm_size = 1;
     void (*comm_free)(void *) = nullptr;   // set by cmpc_comm_init, called by cmpc_destroy
     int plans_B = 0;   // problems whose contact plans were built on the device
+    // per-iteration records and the accepted-iterate history (ensure_history): capacities in
+    // iterations per problem; the K / Sigma slots exist only once GuSTO mode ran
+    void *hlog = nullptr, *hX = nullptr, *hU = nullptr, *hK = nullptr, *hS = nullptr;
+    int log_cap = 0, hist_cap = 0, hks_cap = 0;
     // grow-only device scratch of the host getters (knot-major staging copies)
     void *scratch = nullptr;
     size_t scratch_bytes = 0;
@@ -84,6 +89,16 @@ struct cmpc_handle_s {
         HIPCHK(hipMemsetAsync(p, 0, std::max<size_t>(bytes, 16), stream));
         allocs.push_back(p);
         return p;
+    }
+    // replace a handle allocation by a zeroed one of `bytes` (old contents dropped)
+    void regrow(void *&p, size_t bytes) {
+        if (p) {
+            HIPCHK(hipStreamSynchronize(stream));
+            HIPCHK(hipFree(p));
+            allocs.erase(std::find(allocs.begin(), allocs.end(), p));
+            p = nullptr;
+        }
+        p = dalloc(bytes);
     }
     void *scratch_bytes_at_least(size_t bytes) {
         if (bytes > scratch_bytes) {
@@ -115,6 +130,9 @@ struct cmpc_handle_s {
         d.Xacc = (T *)Xacc; d.Uacc = (T *)Uacc; d.Kacc = (T *)Kacc; d.Sacc = (T *)Sacc;
         d.stamps = (unsigned long long *)stamps;
         d.scan_ctr = nullptr;
+        d.hlog = (cmpc_iter_record *)hlog; d.log_cap = log_cap; d.hist_cap = hist_cap;
+        d.hX = (T *)hX; d.hU = (T *)hU;
+        d.hK = hks_cap >= hist_cap ? (T *)hK : nullptr; d.hS = hks_cap >= hist_cap ? (T *)hS : nullptr;
         return d;
     }
 };
@@ -170,5 +188,10 @@ inline void from_dev_raw(cmpc_handle h, void *dst, const void *src, size_t bytes
     HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
 }
+
+// cmpc_api.cpp: shared by the entry points of every translation unit
+void settle_all(cmpc_handle h);              // run / join a deferred or side-stream covariance scan
+void ensure_dense(cmpc_handle h);            // the dense A, Bu, C of the last linearization
+void materialize_accepted_ks(cmpc_handle h); // accepted K / Sigma out of the live arrays
 
 }  // namespace cmpc_host

@@ -23,6 +23,7 @@
 // point (x_0 on every knot, zero controls).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -216,6 +217,7 @@ extern "C" int cmpc_load_qp(cmpc_handle h, int b, int n, int m, const double *P_
 
         // ---- dynamics rows: decode beta, w, alpha, lever (+ TALOS CoP / torque columns), rebuild, compare
         double beta = 0;
+        std::vector<double> Aem((size_t)81 * N), Bem((size_t)9 * NU * N);   // element-major [e][k], for the getters
         for (int k = 0; k < N; ++k) {
             double Ad[9][9] = {}, Bd[9][NU] = {};
             for (int i = 0; i < 9; ++i) {
@@ -277,6 +279,10 @@ extern "C" int cmpc_load_qp(cmpc_handle h, int b, int n, int m, const double *P_
             for (int i = 0; i < 9; ++i)
                 for (int j = 0; j < NU; ++j)
                     need(close(Bd[i][j], Br[i][j], sb), at("B_k is not of the centroidal form", k, i));
+            for (int i = 0; i < 9; ++i) {
+                for (int j = 0; j < 9; ++j) Aem[(size_t)(i * 9 + j) * N + k] = Ad[i][j];
+                for (int j = 0; j < NU; ++j) Bem[(size_t)(i * NU + j) * N + k] = Bd[i][j];
+            }
         }
         need(beta > 0, "A_0 must carry dt / mass > 0 on the momentum columns");
         prm.mass = prm.dt / beta;
@@ -307,7 +313,14 @@ extern "C" int cmpc_load_qp(cmpc_handle h, int b, int n, int m, const double *P_
         for (int k = 0; k < K1; ++k)
             for (int i = 0; i < 9; ++i) put(S::QX + i, k, q[9 * k + i]);
 
-        // ---- install: a parameter class for this problem, then the device arrays
+        // ---- install: a parameter class for this problem, then the device arrays.
+        // The other problems' accepted K / Sigma leave the live arrays (the class list changes), and
+        // their dense A, Bu are written now from their own linearization points: a later getter or
+        // export must not rerun k_lin_knots, which would rebuild problem b's stage record from the
+        // synthetic starting point below.  Problem b's dense A, Bu are the loaded ones.  A later
+        // cmpc_linearize re-linearizes every problem at its stored point, b included.
+        materialize_accepted_ks(h);
+        ensure_dense(h);
         {
             // an identical class is reused, so repeated loads do not grow the class list
             int32_t cid = -1;
@@ -339,6 +352,19 @@ extern "C" int cmpc_load_qp(cmpc_handle h, int b, int n, int m, const double *P_
         up(h->Xlin, (size_t)b * K1 * 9, xl);
         up(h->Ulin, (size_t)b * N * NU, ul);
         up(h->cw, (size_t)b, std::vector<double>{cw});
+        {   // element e of (b, k) at e * LS + b * N + k
+            const size_t LS = (size_t)h->max_batch * N;
+            std::vector<double> tmp(N);
+            for (int el = 0; el < 81; ++el) {
+                std::copy(&Aem[(size_t)el * N], &Aem[(size_t)el * N] + N, tmp.begin());
+                up(h->A, el * LS + (size_t)b * N, tmp);
+            }
+            for (int el = 0; el < 9 * NU; ++el) {
+                std::copy(&Bem[(size_t)el * N], &Bem[(size_t)el * N] + N, tmp.begin());
+                up(h->Bu, el * LS + (size_t)b * N, tmp);
+            }
+            h->lin_dense = true;
+        }
         HIPCHK(hipMemcpyAsync((char *)h->logic + (size_t)b * N * NC, logic.data(), logic.size(), hipMemcpyHostToDevice,
                               h->stream));
         HIPCHK(hipStreamSynchronize(h->stream));

@@ -20,6 +20,8 @@
 // (field f of knot k at base + f * KPC + k, common.hpp), so each field access of a wave is one
 // contiguous 512-B transaction; per-block vectors (nu, r_e) use the same scheme over the N + 2
 // Schur blocks.  The Schur right-hand side / direction dnu never leave LDS.
+#include <limits>
+
 #include "common.hpp"
 #include "cov_scan.hpp"
 
@@ -406,6 +408,16 @@ template <int n, typename T, typename P> __device__ __forceinline__ void stv(P p
 // then move above the stores, so every result row is stored as soon as it is formed and the
 // phase never holds the whole knot in registers (holding it serialized the loads of late rows
 // behind one memory round trip each).
+// Mixed precision for the fp32 kernels: the residuals are formed in fp64 from the fp32 iterate
+// and records (Acc<float> = double), then rounded once on store.  In fp32 the dual rows of the
+// states sum terms of ~1e3-1e5 (W_x x, q = -W_x xbar, E' nu) that cancel to ~1e-2: fp32 sums left a
+// floor of ~7e-3 on Solo12 trot, above the 1e-6 relative tolerance, so the iteration ran on until
+// mu underflowed (status -10, tests/golden trot_f32).  With exact residuals the Newton steps,
+// still fp32, refine the iterate down to what fp32 can represent, as in mixed-precision iterative
+// refinement.  fp64: Acc<double> = double, the same code as before.
+template <typename T> struct Acc { using type = T; };
+template <> struct Acc<float> { using type = double; };
+
 template <typename T, int ROBOT>
 __device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<T, ROBOT> &nm, const T *__restrict__ stp,
                                            const T *__restrict__ xs, const T *__restrict__ us, const T *__restrict__ ts,
@@ -414,6 +426,7 @@ __device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<
                                            T *__restrict__ rde_o, T *__restrict__ rdi_o) {
     using S = Stage<ROBOT>;
     using R_ = Rows<ROBOT>;
+    using A = typename Acc<T>::type;
     constexpr int NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
     constexpr int ld = KPC;
     const int N = C.N;
@@ -421,7 +434,7 @@ __device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<
     const DevParams<T> &P = *C.prm;
     const SV<const T> st{stp};
     const unsigned msk = C.cmask(k);
-    T x[9], u[NU], x1[9], nk[9], n1[9], w[3];
+    A x[9], u[NU], x1[9], nk[9], n1[9], w[3];
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
         x[i] = xs[i * ld];
@@ -429,79 +442,89 @@ __device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<
         nk[i] = nus[i * ld];      // nu blocks k, k + 1
         n1[i] = nus[i * ld + 1];
     }
+    if (sizeof(T) == 4) {
+        // fp32: the dual scale also counts the multipliers the rows sum.  E' nu = -nu_k + A_k' nu_{k+1}
+        // cancels (Solo12 trot: |nu| ~ 1e5 against |E' nu| ~ 2e3), and |nu| in fp32 alone carries
+        // ~6e-8 |nu| of rounding into every dual row: without this term the 1e-6 relative test sat
+        // below the representable floor (merit 2.4-3 for ever, tests/golden trot_f32).
+        A nmag = A(0);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) nmag = fmax(nmag, fmax(fabs(nk[i]), fabs(n1[i])));
+        nm.sd = fmax(nm.sd, T(nmag));
+    }
 #pragma unroll
     for (int i = 0; i < NU; ++i) u[i] = us[i * ld];   // k = N: padding column (values unused)
     for (int i = 0; i < 3; ++i) w[i] = st[S::W + i];
-    const T t = ts[0];
+    const A t = ts[0], beta = C.beta, cw = C.cw;
     // E' nu at knot k (kept for the dual rows at the end)
-    T ex[9], eu[NU];
+    A ex[9], eu[NU];
     for (int i = 0; i < 9; ++i) ex[i] = (k == 0) ? nk[i] : -nk[i];
     if (k == N) for (int i = 0; i < 9; ++i) ex[i] += n1[i];
     if (hu) {
-        T a[9];
-        opAT(w, C.beta, n1, a);
+        A a[9];
+        opAT(w, beta, n1, a);
         for (int i = 0; i < 9; ++i) ex[i] += a[i];
-        opBT<T, ROBOT>(st, n1, eu);
+        opBT<A, ROBOT>(st, n1, eu);
         // dynamics row block 1 + k first: its loads (x_{k+1}, r_k) are then dead before the rows
-        T ax[9], bu[9];
-        opA(w, C.beta, x, ax);
-        opB<T, ROBOT>(st, u, bu);
+        A ax[9], bu[9];
+        opA(w, beta, x, ax);
+        opB<A, ROBOT>(st, u, bu);
 #pragma unroll
         for (int i = 0; i < 9; ++i) {
-            const T ez = ax[i] + bu[i] - x1[i], r = st[S::R + i];
-            const T re = ez - r;
-            rde_o[i * ld + 1 + k] = re;
-            nm.prim = fmax(nm.prim, fabs(re));
-            nm.sp = fmax(nm.sp, fmax(fabs(ez), fabs(r)));
+            const A ez = ax[i] + bu[i] - x1[i], r = st[S::R + i];
+            const A re = ez - r;
+            rde_o[i * ld + 1 + k] = T(re);
+            nm.prim = fmax(nm.prim, T(fabs(re)));
+            nm.sp = fmax(nm.sp, T(fmax(fabs(ez), fabs(r))));
         }
     }
     if (k == 0 || k == N) {   // boundary rows: block 0 (initial state) / N + 1 (final state)
         const T *xb = C.xbar + (size_t)k * 9;
         for (int i = 0; i < 9; ++i) {
-            const T rb = x[i] - xb[i];
-            rde_o[i * ld + (k == 0 ? 0 : N + 1)] = rb;
-            nm.prim = fmax(nm.prim, fabs(rb));
-            nm.sp = fmax(nm.sp, fmax(fabs(x[i]), fabs(xb[i])));
+            const A rb = x[i] - A(xb[i]);
+            rde_o[i * ld + (k == 0 ? 0 : N + 1)] = T(rb);
+            nm.prim = fmax(nm.prim, T(fabs(rb)));
+            nm.sp = fmax(nm.sp, T(fmax(fabs(x[i]), A(fabs(xb[i])))));
         }
     }
     // inequality rows: r_i = g'z - h + s, complementarity and norms; G' lambda accumulated on the fly
-    T gL[3] = {T(0), T(0), T(0)}, gt = T(0), gu[NU];
+    A gL[3] = {A(0), A(0), A(0)}, gt = A(0), gu[NU];
 #pragma unroll
-    for (int i = 0; i < NU; ++i) gu[i] = T(0);
+    for (int i = 0; i < NU; ++i) gu[i] = A(0);
     // complementarity sums in short per-group chains (one long serial chain made the scheduler
     // keep every row's product live until the end); the row count is exact in integers
     T mug = T(0);
-    auto row = [&](int r, bool pr, T g, T h) {
-        const T v = g - h, sr = ss[r * ld], lr = ls[r * ld];
-        rdi_o[r * ld] = pr ? v + sr : T(0);
-        const T c = pr ? sr * lr : T(0);
-        nm.prim = fmax(nm.prim, pr ? v : T(0));
-        nm.sp = fmax(nm.sp, pr ? fmax(fabs(g), fabs(g - v)) : T(0));
+    auto row = [&](int r, bool pr, A g, A h) {
+        const A v = g - h, sr = ss[r * ld], lr = ls[r * ld];
+        rdi_o[r * ld] = pr ? T(v + sr) : T(0);
+        const T c = pr ? T(sr * lr) : T(0);
+        nm.prim = fmax(nm.prim, pr ? T(v) : T(0));
+        nm.sp = fmax(nm.sp, pr ? T(fmax(fabs(g), fabs(g - v))) : T(0));
         nm.comp = fmax(nm.comp, c);
         mug += c;
-        nm.lmax = fmax(nm.lmax, pr ? lr : T(0));
-        return pr ? lr : T(0);
+        nm.lmax = fmax(nm.lmax, pr ? T(lr) : T(0));
+        return pr ? lr : A(0);
     };
     nm.cnt += T(9 + (hu ? 4 * (1 + Robot<ROBOT>::COP) * __builtin_popcount(msk) : 0));
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        const T g = tr_sign<T>(j, 0) * x[6] + tr_sign<T>(j, 1) * x[7] + tr_sign<T>(j, 2) * x[8] + C.cw * t;
-        const T lr = row(j, true, g, st[S::BTR + j]);
-        for (int i = 0; i < 3; ++i) gL[i] += tr_sign<T>(j, i) * lr;
-        gt += C.cw * lr;
+        const A g = tr_sign<A>(j, 0) * x[6] + tr_sign<A>(j, 1) * x[7] + tr_sign<A>(j, 2) * x[8] + cw * t;
+        const A lr = row(j, true, g, st[S::BTR + j]);
+        for (int i = 0; i < 3; ++i) gL[i] += tr_sign<A>(j, i) * lr;
+        gt += cw * lr;
     }
-    gt -= row(8, true, -t, T(0));
+    gt -= row(8, true, -t, A(0));
     nm.mu += mug;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         mug = T(0);
         const bool pr = hu && ((msk >> c) & 1u);
         const auto cs = st + (S::CON + S::CS * c);
-        const T *f = u + NUPC * c + FO;
+        const A *f = u + NUPC * c + FO;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const T g0 = cs[S::G + 3 * r], g1 = cs[S::G + 3 * r + 1], g2 = cs[S::G + 3 * r + 2];
-            const T lr = row(R_::FR + 4 * c + r, pr, g0 * f[0] + g1 * f[1] + g2 * f[2], cs[S::H + r]);
+            const A g0 = cs[S::G + 3 * r], g1 = cs[S::G + 3 * r + 1], g2 = cs[S::G + 3 * r + 2];
+            const A lr = row(R_::FR + 4 * c + r, pr, g0 * f[0] + g1 * f[1] + g2 * f[2], cs[S::H + r]);
             gu[NUPC * c + FO] += g0 * lr;
             gu[NUPC * c + FO + 1] += g1 * lr;
             gu[NUPC * c + FO + 2] += g2 * lr;
@@ -510,8 +533,8 @@ __device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<
 #pragma unroll
             for (int q = 0; q < 4; ++q) {   // cop <= hi | -cop <= -lo (lo = -(lxn | lyn))
                 const int dd = q / 2;
-                const T cop = u[NUPC * c + dd];
-                const T lr = (q % 2 == 0) ? row(R_::CP + 4 * c + q, pr, cop, P.foot_range[dd == 0 ? 0 : 2])
+                const A cop = u[NUPC * c + dd];
+                const A lr = (q % 2 == 0) ? row(R_::CP + 4 * c + q, pr, cop, P.foot_range[dd == 0 ? 0 : 2])
                                           : row(R_::CP + 4 * c + q, pr, -cop, P.foot_range[dd == 0 ? 1 : 3]);
                 gu[NUPC * c + dd] += (q % 2 == 0) ? lr : -lr;
             }
@@ -520,25 +543,25 @@ __device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<
     }
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
-        const T hx = C.Wx(i) * x[i], q = st[S::QX + i];
-        const T g = (i >= 6) ? gL[i - 6] : T(0);
-        const T rd = hx + q + ex[i] + g;
-        rdx_o[i * ld] = rd;
-        nm.dual = fmax(nm.dual, fabs(rd));
-        nm.sd = fmax(nm.sd, fmax(fabs(hx), fmax(fabs(q), fmax(fabs(ex[i]), fabs(g)))));
+        const A hx = A(C.Wx(i)) * x[i], q = st[S::QX + i];
+        const A g = (i >= 6) ? gL[i - 6] : A(0);
+        const A rd = hx + q + ex[i] + g;
+        rdx_o[i * ld] = T(rd);
+        nm.dual = fmax(nm.dual, T(fabs(rd)));
+        nm.sd = fmax(nm.sd, T(fmax(fabs(hx), fmax(fabs(q), fmax(fabs(ex[i]), fabs(g))))));
     }
-    const T rdt = T(1) + gt;
-    rdt_o[0] = rdt;
-    nm.dual = fmax(nm.dual, fabs(rdt));
+    const A rdt = A(1) + gt;
+    rdt_o[0] = T(rdt);
+    nm.dual = fmax(nm.dual, T(fabs(rdt)));
     nm.sd = fmax(nm.sd, T(1));
     if (hu) {
 #pragma unroll
         for (int i = 0; i < NU; ++i) {
-            const T h = C.Wu(i) * u[i];
-            const T rd = h + eu[i] + gu[i];
-            rdu_o[i * ld] = rd;
-            nm.dual = fmax(nm.dual, fabs(rd));
-            nm.sd = fmax(nm.sd, fmax(fabs(h), fmax(fabs(eu[i]), fabs(gu[i]))));
+            const A h = A(C.Wu(i)) * u[i];
+            const A rd = h + eu[i] + gu[i];
+            rdu_o[i * ld] = T(rd);
+            nm.dual = fmax(nm.dual, T(fabs(rd)));
+            nm.sd = fmax(nm.sd, T(fmax(fabs(h), fmax(fabs(eu[i]), fabs(gu[i])))));
         }
     }
 }
@@ -2134,7 +2157,7 @@ __global__ void __launch_bounds__(NTT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int o
             if (corr == 0) {   // Mehrotra centering from the affine step's complementarity
                 block_reduce<T, NTT, 3, 0>(mus, red);
                 const T mu_aff = (mus[0] + alpha * (mus[1] + alpha * mus[2])) / fmax(sm2[1], T(1));
-                const T sg = mu_aff / fmax(mu, T(1e-300));
+                const T sg = mu_aff / fmax(mu, std::numeric_limits<T>::min());
                 sigma_mu = sg * sg * sg * mu;
             } else if ((alpha < T(QP_REFINE_ALPHA) || stall > 0) && merit < T(QP_REFINE_MERIT)) {
                 // the step collapsed, or mu did not halve in the last iteration, late in the solve:

@@ -235,6 +235,7 @@ __global__ void __launch_bounds__(ACC_NT) k_accept(DevBuf<T> d, int fixed_iters)
     }
     if (tid == 0) {
         int dec;
+        const double w_it = sc.weight, r_it = sc.radius;   // the trust region this iteration's QP ran with
         sc.qp_status = qst;
         sc.qp_iters = d.qp_iters[b];
         sc.tr_norm = tr;
@@ -259,6 +260,13 @@ __global__ void __launch_bounds__(ACC_NT) k_accept(DevBuf<T> d, int fixed_iters)
             dec = DEC_REJECT_TR;
         }
         sc.decision = dec;
+        if (d.hlog && sc.iter < d.log_cap) {
+            cmpc_iter_record rec;
+            rec.weight = w_it; rec.radius = r_it; rec.tr_norm = tr;
+            rec.rho = (dec == DEC_ACCEPT || dec == DEC_REJECT_RHO) ? rho : __builtin_nan("");
+            rec.iteration = sc.iter; rec.qp_status = qst; rec.qp_iters = sc.qp_iters; rec.decision = dec;
+            d.hlog[(size_t)b * d.log_cap + sc.iter] = rec;
+        }
         sc.iter += 1;
         if (dec == DEC_QP_FAILED) {
             sc.status = CMPC_SCP_QP_FAILED;
@@ -295,21 +303,33 @@ __global__ void __launch_bounds__(256) k_keep_accepted(DevBuf<T> d) {
     const bool gusto = d.scp_mode == CMPC_SCP_MODE_GUSTO;
     const T *Xs = d.xs + (size_t)b * nx, *Us = d.us + (size_t)b * nu;
     const int ne = nx + nu + (d.copy_ks ? nk + ns : 0);
+    // history slot of this accept (the reference appends every accepted iterate)
+    const int slot = d.scp[b].n_accepted - 1;
+    const bool hist = d.hX && slot >= 0 && slot < d.hist_cap;
+    const size_t Bm = d.LS / N;   // max_batch
     for (int e = blockIdx.x * 256 + threadIdx.x; e < ne; e += gridDim.x * 256) {
         if (e < nx) {
-            d.Xacc[(size_t)b * nx + e] = Xs[e];
-            if (gusto) d.Xlin[(size_t)b * nx + e] = Xs[e];
+            const T v = Xs[e];
+            d.Xacc[(size_t)b * nx + e] = v;
+            if (gusto) d.Xlin[(size_t)b * nx + e] = v;
+            if (hist) d.hX[((size_t)slot * Bm + b) * nx + e] = v;
         } else if (e < nx + nu) {
             const int i = e - nx;
-            d.Uacc[(size_t)b * nu + i] = Us[i];
-            if (gusto) d.Ulin[(size_t)b * nu + i] = Us[i];
+            const T v = Us[i];
+            d.Uacc[(size_t)b * nu + i] = v;
+            if (gusto) d.Ulin[(size_t)b * nu + i] = v;
+            if (hist) d.hU[((size_t)slot * Bm + b) * nu + i] = v;
         } else if (e < nx + nu + nk) {   // element-major, like K
             const int i = e - nx - nu;
             const size_t j = (size_t)(i / N) * d.LS + (size_t)b * N + i % N;
-            d.Kacc[j] = d.K[j];
+            const T v = d.K[j];
+            d.Kacc[j] = v;
+            if (hist && d.hK) d.hK[(size_t)slot * (NU * 9) * d.LS + j] = v;
         } else {
             const size_t j = (size_t)b * ns + (e - nx - nu - nk);
-            d.Sacc[j] = d.Sig[j];
+            const T v = d.Sig[j];
+            d.Sacc[j] = v;
+            if (hist && d.hS) d.hS[(size_t)slot * Bm * ns + j] = v;
         }
     }
 }

@@ -17,7 +17,7 @@ libcmpc.so on the GPU:
   refused with a ``CmpcError`` naming the offending row.
 
 The reference's OSQP call (eps 1e-7 + polish, src/scp_solver.py:59-68) is replaced by an
-interior-point method converged to 1e-11 (fp64): the QP's minimizer is unique (P > 0 on the
+interior-point method converged to 1e-10 (fp64; 1e-6 fp32): the QP's minimizer is unique (P > 0 on the
 states and controls, slacks priced linearly), so both return the same solution to within the
 reference's own tolerance.
 """
@@ -167,44 +167,72 @@ def interpolate_SCP_solution(solution):
     return dict(X=interp(X), U=interp(U))
 
 
-def _results(sol, nu, B):
+def _results(s, sol, nu, B):
+    """The reference's dict of lists per problem: every accepted iterate in acceptance order
+    (src/scp_solver.py:162-167; the device keeps them, cmpc_get_accepted), or False (QP failed)."""
     out = []
+    n_acc = sol['n_accepted']
+    per = [s.accepted(j) for j in range(int(n_acc.max()) if B else 0)]
     for b in range(B):
         if int(sol['status'][b]) == SCP_QP_FAILED:
             out.append(False)
             continue
         r = dict(state=[], control=[], gains=[], covs=[])
-        if int(sol['n_accepted'][b]) > 0:
-            r['state'].append(sol['X'][b].T.copy())
-            r['control'].append(sol['U'][b][:, :nu].T.copy())
-            r['gains'].append(sol['K'][b][:, :nu, :].copy())
-            r['covs'].append(sol['Sigma'][b].copy())
+        for j in range(int(n_acc[b])):
+            a = per[j]
+            r['state'].append(a['X'][b].T.copy())
+            r['control'].append(a['U'][b][:, :nu].T.copy())
+            r['gains'].append(a['K'][b][:, :nu, :].copy())
+            r['covs'].append(a['Sigma'][b].copy())
         out.append(r)
     return out
 
 
-def solve_scp(model, scp_params, gusto=False):
+def _print_iterations(records, n):
+    """The reference's per-iteration banners and decisions (src/scp_solver.py:135-178), from the
+    device's iteration records."""
+    for rec in records[:n]:
+        print('\n' + '=' * 50)
+        print('Iteration ' + str(int(rec['iteration'])))
+        print('-' * 50)
+        dec = int(rec['decision'])
+        if dec == -1:
+            print('QP subproblem Failed at iter #' + str(int(rec['iteration'])))
+        elif dec == 3:
+            print('solution is outside trust region .. rejecting solution and increasing trust region weight')
+        else:
+            print('solution is inside trust region .. checking model accuracy')
+            print("error ratio between linearized and nonlinear dynamics = ", float(rec['rho']))
+            if dec == 2:
+                print('linearized model is NOT accurate .. rejecting solution and decreasing trust region radius')
+            else:
+                print('linearized model is accurate enough .. accepting solution ')
+
+
+def solve_scp(model, scp_params, gusto=False, verbose=True):
     """The reference's SCP loop for one model (reference :118-179), run on the device.
     ``gusto=True`` moves the linearization point to each accepted solution and iterates until
     convergence (the GuSTO scheme the reference cites, :113-117; include/cmpc.h
     CMPC_SCP_MODE_GUSTO); the default reproduces the reference exactly (quirk Q1).
 
-    Returns the reference's dict of lists (state, control, gains, covs).  In reference mode the
-    loop ends at the first accepted iterate (Q1), so the lists hold exactly the reference's one
-    entry.  With ``gusto=True`` several iterates can be accepted; only the final one is returned
-    (the device keeps one accepted iterate per problem), where the reference's loop would append
-    each of them."""
+    Returns the reference's dict of lists (state, control, gains, covs), one entry per accepted
+    iterate in acceptance order, or False when a QP fails.  In reference mode the loop ends at the
+    first accepted iterate (Q1), so the lists hold the reference's one entry; with ``gusto=True``
+    every accepted iterate is returned, as the reference's loop appends them.  ``verbose`` prints
+    the reference's per-iteration banners from the device's iteration records."""
     s = model._device_solver(None, scp_params)
     s.set_scp_mode('gusto' if gusto else 'reference')
     s.solve_scp(fixed_iters=False)
     sol = s.solution()
-    log = s.iteration_log()
-    res = _results(sol, model._n_u, 1)[0]
+    rec, n = s.iteration_history()
+    if verbose:
+        _print_iterations(rec[0], int(n[0]))
+    res = _results(s, sol, model._n_u, 1)[0]
     it = int(sol['iterations'][0])
     if res is False:
-        print('QP subproblem Failed at iter #' + str(it - 1))
         return False
-    print('[solve_ccscp] Success: ' + str(int(log['decision'][0]) == 1) + ', Nb of iterations: ' + str(it))
+    print('[solve_ccscp] Success: ' + str(int(rec[0][n[0] - 1]['decision']) == 1 if n[0] else False)
+          + ', Nb of iterations: ' + str(it))
     return res
 
 
@@ -240,7 +268,7 @@ def solve_scp_batch(models, scp_params=None, precision='fp64', device=0, fixed_i
         s.solve_scp(fixed_iters=fixed_iters)
         sol = s.solution()
         interp = s.interpolate(int(n_inner)) if n_inner else None
-    res = _results(sol, m0._n_u, batch.B)
+        res = _results(s, sol, m0._n_u, batch.B)
     if interp is not None:
         for b, r in enumerate(res):
             if r is not False and r['state']:

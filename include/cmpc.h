@@ -124,6 +124,7 @@ typedef struct {
     float linearize_ms, assemble_ms, qp_ms, accept_ms, total_ms;
 } cmpc_timing;
 
+/* Returns -2 for invalid sizes, -5 for TALOS in fp32 (unsupported: its QPs need fp64). */
 int cmpc_create(cmpc_handle *out, int device, int robot, int N, int max_batch, int precision);
 int cmpc_destroy(cmpc_handle h);
 const char *cmpc_last_error(cmpc_handle h);
@@ -224,8 +225,33 @@ int cmpc_get_qp_info(cmpc_handle h, double *merit, int32_t *n_refine);
  * arrays).  GuSTO mode and new contact plans copy them per accept. */
 int cmpc_get_solution(cmpc_handle h, double *X, double *U, double *K, double *Sigma, int32_t *n_accepted,
                       int32_t *iterations, int32_t *scp_status, double *weight, double *radius);
+/* The last iteration of each problem (B entries each; NULL skips). */
 int cmpc_get_iteration_log(cmpc_handle h, double *tr_norm, double *rho, int32_t *qp_status,
                            int32_t *qp_iters, int32_t *decision);
+
+/* One SCP iteration of one problem: what the reference prints per iteration
+ * (src/scp_solver.py:135-178, banners and decisions) and the trust region it ran with. */
+#define CMPC_DECISION_ACCEPT 1
+#define CMPC_DECISION_REJECT_RHO 2   /* inside the trust region, rho > rho1: radius *= beta_fail */
+#define CMPC_DECISION_REJECT_TR 3    /* outside the trust region: weight *= gamma_fail */
+#define CMPC_DECISION_QP_FAILED (-1) /* the reference returns False */
+typedef struct {
+    double weight, radius;   /* trust-region weight / radius of this iteration's QP */
+    double tr_norm;          /* ||X_sol - X_lin||_2 (spectral norm, quirk Q6) */
+    double rho;              /* model-accuracy ratio; NaN where the reference does not evaluate it */
+    int32_t iteration, qp_status, qp_iters, decision;
+} cmpc_iter_record;
+/* Every SCP iteration of every problem since its upload, in order: records (B, cap), iteration i
+ * of problem b at records[b * cap + i]; n_records (B) = iterations recorded.  The device keeps
+ * max(max_iterations) records per problem (the larger of the parameter classes'); iterations
+ * beyond it (fixed-K runs past max_iterations) are not recorded.  cap may be any size >= 1. */
+int cmpc_get_iteration_history(cmpc_handle h, int cap, cmpc_iter_record *records, int32_t *n_records);
+/* Accepted iterate j (0-based, in acceptance order) of every problem: X (B,N+1,9), U (B,N,nu),
+ * K (B,N,nu,9), Sigma (B,N+1,9,9) (NULL skips); zeros for problems with fewer than j + 1 accepted
+ * iterates.  The reference appends every accepted iterate to its lists (src/scp_solver.py:162-167);
+ * the device keeps up to max(max_iterations) per problem.  Reference mode: K and Sigma are those of
+ * the (fixed) linearization point, bit-identical for every iterate (quirk Q1). */
+int cmpc_get_accepted(cmpc_handle h, int j, double *X, double *U, double *K, double *Sigma);
 /* Current linearization point (B,N+1,9) / (B,N,nu) and the last convergence measure
  * ||dU||/||U|| + ||dX||/||X|| of each problem (0 in reference mode, quirk Q1). */
 int cmpc_get_linearization_point(cmpc_handle h, double *X, double *U, double *convergence);

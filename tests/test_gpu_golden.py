@@ -85,7 +85,10 @@ def test_exported_qp_equals_reference_matrices(tag, which, golden):
     P, q, A, l, u = s.export_qp(0)
     s.close()
     assert abs(P - golden_P(g)).max() == 0.0
-    np.testing.assert_allclose(q, g['q'], rtol=1e-14, atol=1e-14)
+    if golden_fp32(g):   # the device forms q = -Wx xbar in float32
+        _close(q, g['q'], 2e-7)
+    else:
+        np.testing.assert_allclose(q, g['q'], rtol=1e-14, atol=1e-14)
     A0, l0, u0 = golden_csc(g, which)
     assert A.shape == A0.shape
     if golden_fp32(g):

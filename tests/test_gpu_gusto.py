@@ -108,3 +108,83 @@ def test_accepted_gains_and_covariances_survive_mode_switch():
         np.testing.assert_array_equal(sol3['n_accepted'], sol['n_accepted'])
         np.testing.assert_array_equal(sol3['K'], sol['K'])
         np.testing.assert_array_equal(sol3['Sigma'], sol['Sigma'])
+
+
+@pytest.mark.parametrize('cfg,N,B', [('trot', 30, 3), ('bound', 30, 2)])
+def test_gusto_accepted_history_matches_oracle(cfg, N, B):
+    """Every accepted iterate, in acceptance order (the reference appends each one,
+    src/scp_solver.py:162-167): list lengths equal the oracle's GuSTO loop's, and each accepted X,
+    U, K, Sigma matches it (X, U 1e-5 of scale; K, Sigma 1e-5 relative: they are linearized at
+    the previous accepted X, U, so they inherit the QP's 1e-10-level differences, amplified by the
+    Riccati steps).  The drop-in's solve_scp_batch returns the same lists."""
+    pb = make_batch(cfg, N, B)
+    with Solver(pb.robot, N, B, 'fp64') as s:
+        s.upload(pb)
+        s.set_scp_mode('gusto')
+        s.solve_scp(fixed_iters=False)
+        sol = s.solution()
+        acc = [s.accepted(j) for j in range(int(sol['n_accepted'].max()))]
+        rec, nrec = s.iteration_history()
+    multi = 0
+    for b in range(B):
+        p = pb.oracle_problem(b)
+        log = []
+        ref = OS.solve_scp(p, p['scp_params'], qp=sparse_ipm_qp, log=log, gusto=True)
+        assert ref is not False and int(sol['n_accepted'][b]) == len(ref['state'])
+        multi += len(ref['state']) > 1
+        for j in range(len(ref['state'])):
+            X, U, K, S = ref['state'][j], ref['control'][j], ref['gains'][j], ref['covs'][j]
+            np.testing.assert_allclose(acc[j]['X'][b].T, X, rtol=0, atol=1e-5 * np.abs(X).max())
+            np.testing.assert_allclose(acc[j]['U'][b][:, :U.shape[0]].T, U, rtol=0, atol=1e-5 * np.abs(U).max())
+            np.testing.assert_allclose(acc[j]['K'][b][:, :K.shape[1]], K, rtol=0, atol=1e-5 * np.abs(K).max())
+            np.testing.assert_allclose(acc[j]['Sigma'][b], S, rtol=0, atol=1e-5 * np.abs(S).max())
+        for j in range(len(ref['state']), len(acc)):   # beyond this problem's accepts: zeros
+            assert not acc[j]['X'][b].any()
+        # one record per iteration, the oracle's decisions, trust regions and norms
+        assert int(nrec[b]) == len(log)
+        code = {'accept': 1, 'reject_rho': 2, 'reject_tr': 3}
+        for i, r in enumerate(log):
+            d = rec[b][i]
+            assert int(d['iteration']) == i and int(d['decision']) == code[r['decision']]
+            assert abs(d['weight'] - r['weight']) <= 1e-12 * r['weight']
+            assert abs(d['radius'] - r['radius']) <= 1e-12 * r['radius']
+            assert abs(d['tr_norm'] - r['tr_norm']) <= 1e-5 * max(1.0, r['tr_norm'])
+            if 'rho' in r:
+                assert abs(d['rho'] - r['rho']) <= 1e-5 * max(1e-6, abs(r['rho']))
+            else:
+                assert np.isnan(d['rho'])
+    assert multi >= 1
+
+
+def test_reference_mode_iteration_history_with_rejects():
+    """Reference mode with a radius small enough that the first iterations reject (trust-region
+    rejects raise the weight, rho rejects halve the radius): the per-iteration records equal the
+    oracle's log of the reference's state machine, and the single accepted iterate is history
+    slot 0 (= cmpc_get_solution)."""
+    N, B = 30, 3
+    pb = make_batch('trot', N, B)
+    for p in pb.params:
+        p.scp_params = dict(p.scp_params, trust_region_radius0=0.05)
+    with Solver(pb.robot, N, B, 'fp64') as s:
+        s.upload(pb)
+        s.solve_scp(fixed_iters=False)
+        sol = s.solution()
+        rec, nrec = s.iteration_history()
+        a0 = s.accepted(0)
+    code = {'accept': 1, 'reject_rho': 2, 'reject_tr': 3}
+    saw_reject = 0
+    for b in range(B):
+        p = pb.oracle_problem(b)
+        log = []
+        OS.solve_scp(p, p['scp_params'], qp=sparse_ipm_qp, log=log)
+        assert int(nrec[b]) == len(log) == int(sol['iterations'][b])
+        saw_reject += sum(r['decision'] != 'accept' for r in log)
+        for i, r in enumerate(log):
+            d = rec[b][i]
+            assert int(d['decision']) == code[r['decision']], (b, i, d, r)
+            assert abs(d['weight'] - r['weight']) <= 1e-12 * r['weight']
+            assert abs(d['radius'] - r['radius']) <= 1e-12 * r['radius']
+        if sol['n_accepted'][b]:
+            np.testing.assert_array_equal(a0['X'][b], sol['X'][b])
+            np.testing.assert_array_equal(a0['K'][b], sol['K'][b])
+    assert saw_reject >= 1

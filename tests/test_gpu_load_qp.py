@@ -139,3 +139,40 @@ def test_dropin_solve_subproblem_on_plain_tuples():
     ref = sparse_ipm_qp(P, q, A, l, u)
     nxu = 9 * 31 + 12 * 30
     assert np.abs(res.x[:nxu] - ref.x[:nxu]).max() <= 1e-5 * np.abs(ref.x[:nxu]).max()
+
+
+@pytest.mark.parametrize('cfg,N', [('trot', 30), ('talos', 40)])
+def test_load_after_linearize_then_export(cfg, N):
+    """Loading into a handle that has already linearized (reference mode: the stage record is
+    written, the dense A, Bu are not) must not let a later export or getter rerun the
+    linearization over the loaded problem: the export of problem 1 equals the QP loaded into it,
+    problem 0's export is unchanged, and the next QP solve solves the loaded QP."""
+    pb = make_batch(cfg, N, 2, seed_offset=9)
+    s = Solver(pb.robot, N, 2, 'fp64')
+    s.upload(pb)
+    s.linearize(); s.assemble()
+    _, p, qp = _ref_qp(cfg, N, b=3, radius=0.5)
+    qp0 = s.export_qp(0)
+    s.load_qp(1, *qp)
+    P1, q1, A1, l1, u1 = s.export_qp(1)
+    P0, q0, A0, l0, u0 = s.export_qp(0)
+    lin = s.linearization()
+    s.qp_solve()
+    z, _, st, _ = s.qp_solution(with_y=False)
+    s.close()
+    P, q, A, l, u = qp
+    assert abs(P1 - P).max() == 0.0 and np.abs(q1 - q).max() <= 1e-12 * np.abs(q).max()
+    assert abs(A1 - A).max() <= 1e-12 * abs(A).max()
+    fin = np.isfinite(u)
+    assert np.array_equal(np.isfinite(u1), fin) and np.abs(u1[fin] - u[fin]).max() <= 1e-9 * (1 + np.abs(u[fin]).max())
+    for a, b_ in zip((P0, A0), (qp0[0], qp0[2])):
+        assert abs(a - b_).max() == 0.0
+    assert np.array_equal(q0, qp0[1])
+    # the getter's dense A of the loaded problem is the loaded one
+    Adyn = A.tocsr()[9:9 + 9 * N][:, :9 * (N + 1)].toarray()
+    for k in (0, N // 2, N - 1):
+        assert np.abs(lin['A'][1][k] - Adyn[9 * k:9 * k + 9, 9 * k:9 * k + 9]).max() <= 1e-12
+    ref = sparse_ipm_qp(*qp)
+    nx = 9 * (N + 1)
+    assert st[1] == 1
+    assert np.abs(z[1][:nx] - ref.x[:nx]).max() / np.abs(ref.x[:nx]).max() <= 1e-5
