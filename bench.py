@@ -262,7 +262,7 @@ def main():
     _, _, qst, _ = solver.qp_solution(with_y=False)
     merit, nref = solver.qp_info()
     gather_ms = None
-    if comm is not None and units_step == nb * world:   # the RCCL gather sends equal slices
+    if comm is not None:   # the accepted solutions of every slice to rank 0 (uneven slices padded)
         comm.barrier()
         tg = time.perf_counter()
         comm.gather_solution(root=0)

@@ -173,11 +173,15 @@ class RcclComm:
         self.allreduce_max([0.0])
 
     def gather_solution(self, root=0):
-        """Every rank's accepted X (B, N+1, 9), U (B, N, 12) and statuses on root (global order);
-        None on the other ranks."""
+        """Every rank's accepted X (B_r, N+1, 9), U (B_r, N, 12) and statuses on root, concatenated
+        in rank order (= the global order of contiguous slices, of any sizes); None elsewhere."""
         B, N, G = self.s.B, self.s.N, self.world
         is_root = self.rank == root
-        tot = G * B if is_root else 0
+        sizes = np.zeros(G)
+        sizes[self.rank] = B
+        tot = int(self.allreduce_max(sizes).sum()) if is_root else 0   # slices may differ in size
+        if not is_root:
+            self.allreduce_max(sizes)
         X = np.zeros((tot, N + 1, 9)); U = np.zeros((tot, N, 12))
         st = np.zeros(tot, np.int32); it = np.zeros(tot, np.int32); qs = np.zeros(tot, np.int32)
         ptr = (lambda a: a.ctypes.data_as(ctypes.c_void_p)) if is_root else (lambda a: None)

@@ -120,56 +120,70 @@ int cmpc_comm_gather_solution(cmpc_handle h, int root, double *X, double *U, int
         ncclComm_t c = comm_of(h);
         need(root >= 0 && root < h->comm_size, "invalid root");
         need(h->B > 0, "no problems uploaded");
-        const int G = h->comm_size;
-        const bool is_root = h->comm_rank == root;
-        // every rank must hold the same batch size (ncclGather sends equal counts)
+        const int G = h->comm_size, rank = h->comm_rank;
+        const bool is_root = rank == root;
+        // every rank's batch size (slices of ceil(B / G) leave the last ranks short): ncclGather
+        // sends equal counts, so each rank sends its slice padded to the largest and the root
+        // packs the blocks back to back (rank-major = the global order of contiguous slices)
+        std::vector<double> bs(G, 0.0);
+        bs[rank] = double(h->B);
         {
-            double bb[2] = {double(h->B), -double(h->B)};
-            DevTmp d(sizeof(bb));
-            HIPCHK(hipMemcpyAsync(d.p, bb, sizeof(bb), hipMemcpyHostToDevice, h->stream));
-            NCCLCHK(ncclAllReduce(d.p, d.p, 2, ncclFloat64, ncclMax, c, h->stream));
-            HIPCHK(hipMemcpyAsync(bb, d.p, sizeof(bb), hipMemcpyDeviceToHost, h->stream));
+            DevTmp d(G * sizeof(double));
+            HIPCHK(hipMemcpyAsync(d.p, bs.data(), G * sizeof(double), hipMemcpyHostToDevice, h->stream));
+            NCCLCHK(ncclAllReduce(d.p, d.p, (size_t)G, ncclFloat64, ncclMax, c, h->stream));
+            HIPCHK(hipMemcpyAsync(bs.data(), d.p, G * sizeof(double), hipMemcpyDeviceToHost, h->stream));
             HIPCHK(hipStreamSynchronize(h->stream));
-            need(bb[0] == -bb[1], "ranks hold different batch sizes (pad the slices)");
         }
+        size_t Bmax = 0;
+        for (double v : bs) Bmax = std::max(Bmax, (size_t)v);
         const size_t B = h->B, N = h->N, e = h->esz();
-        const size_t nx = B * (N + 1) * 9, nu = B * N * NU;
+        const size_t px = (N + 1) * 9, pu = N * NU;   // per problem
         const ncclDataType_t dt = h->prec == CMPC_PREC_F64 ? ncclFloat64 : ncclFloat32;
-        // per-problem integers packed on the device: scp status | SCP iterations | QP status
+        // per-problem integers: scp status | SCP iterations | QP status, padded to Bmax
         std::vector<ScpState> st(B);
         from_dev_raw(h, st.data(), h->scp, B * sizeof(ScpState));
-        std::vector<int32_t> iv(3 * B);
+        std::vector<int32_t> iv(3 * Bmax, 0);
         for (size_t b = 0; b < B; ++b) {
             iv[b] = st[b].status;
-            iv[B + b] = st[b].iter;
-            iv[2 * B + b] = st[b].qp_status;
+            iv[Bmax + b] = st[b].iter;
+            iv[2 * Bmax + b] = st[b].qp_status;
         }
-        DevTmp di(iv.size() * 4);
+        DevTmp di(iv.size() * 4), sx(Bmax * px * e), su(Bmax * pu * e);
         HIPCHK(hipMemcpyAsync(di.p, iv.data(), iv.size() * 4, hipMemcpyHostToDevice, h->stream));
-        DevTmp rx(is_root ? G * nx * e : 16), ru(is_root ? G * nu * e : 16), ri(is_root ? G * iv.size() * 4 : 16);
+        HIPCHK(hipMemsetAsync(sx.p, 0, Bmax * px * e, h->stream));
+        HIPCHK(hipMemsetAsync(su.p, 0, Bmax * pu * e, h->stream));
+        HIPCHK(hipMemcpyAsync(sx.p, h->Xacc, B * px * e, hipMemcpyDeviceToDevice, h->stream));
+        HIPCHK(hipMemcpyAsync(su.p, h->Uacc, B * pu * e, hipMemcpyDeviceToDevice, h->stream));
+        DevTmp rx(is_root ? G * Bmax * px * e : 16), ru(is_root ? G * Bmax * pu * e : 16),
+            ri(is_root ? G * iv.size() * 4 : 16);
         NCCLCHK(ncclGroupStart());
-        NCCLCHK(ncclGather(h->Xacc, rx.p, nx, dt, root, c, h->stream));
-        NCCLCHK(ncclGather(h->Uacc, ru.p, nu, dt, root, c, h->stream));
+        NCCLCHK(ncclGather(sx.p, rx.p, Bmax * px, dt, root, c, h->stream));
+        NCCLCHK(ncclGather(su.p, ru.p, Bmax * pu, dt, root, c, h->stream));
         NCCLCHK(ncclGather(di.p, ri.p, iv.size(), ncclInt32, root, c, h->stream));
         NCCLCHK(ncclGroupEnd());
         HIPCHK(hipStreamSynchronize(h->stream));
         if (!is_root) return;
-        if (h->prec == CMPC_PREC_F64) {
-            from_dev<double>(h, X, rx.p, G * nx);
-            from_dev<double>(h, U, ru.p, G * nu);
-        } else {
-            from_dev<float>(h, X, rx.p, G * nx);
-            from_dev<float>(h, U, ru.p, G * nu);
-        }
         std::vector<int32_t> all(G * iv.size());
         from_dev_raw(h, all.data(), ri.p, all.size() * 4);
-        for (int g = 0; g < G; ++g)
-            for (size_t b = 0; b < B; ++b) {
-                const int32_t *blk = &all[(size_t)g * 3 * B];
-                if (scp_status) scp_status[g * B + b] = blk[b];
-                if (iterations) iterations[g * B + b] = blk[B + b];
-                if (qp_status) qp_status[g * B + b] = blk[2 * B + b];
+        size_t off = 0;
+        for (int g = 0; g < G; ++g) {
+            const size_t Bg = (size_t)bs[g];
+            auto dl = [&](double *dst, const DevTmp &src, size_t per) {
+                if (!dst || Bg == 0) return;
+                const char *blk = (const char *)src.p + (size_t)g * Bmax * per * e;
+                if (h->prec == CMPC_PREC_F64) from_dev<double>(h, dst + off * per, blk, Bg * per);
+                else from_dev<float>(h, dst + off * per, blk, Bg * per);
+            };
+            dl(X, rx, px);
+            dl(U, ru, pu);
+            const int32_t *blk = &all[(size_t)g * 3 * Bmax];
+            for (size_t b = 0; b < Bg; ++b) {
+                if (scp_status) scp_status[off + b] = blk[b];
+                if (iterations) iterations[off + b] = blk[Bmax + b];
+                if (qp_status) qp_status[off + b] = blk[2 * Bmax + b];
             }
+            off += Bg;
+        }
     });
 }
 

@@ -288,9 +288,10 @@ int cmpc_comm_bcast_params(cmpc_handle h, int root, int n_classes, cmpc_params *
 /* In-place elementwise max over ranks of n doubles (also the barrier of the timed region). */
 int cmpc_comm_allreduce_max(cmpc_handle h, double *v, int n);
 /* Gather every rank's accepted solutions and per-problem statuses to root, rank-major (= the
- * global problem order of contiguous slices).  All ranks must hold the same batch size B; root's
- * buffers hold nranks * B problems: X (.., N+1, 9), U (.., N, nu), scp_status, iterations,
- * qp_status (NULL skips).  Non-root ranks may pass NULL. */
+ * global problem order of contiguous slices).  Ranks may hold different batch sizes B_r (the
+ * last slices of ceil(B / G) are short); root's buffers hold the global batch sum_r B_r:
+ * X (.., N+1, 9), U (.., N, nu), scp_status, iterations, qp_status (NULL skips).  Non-root ranks
+ * may pass NULL. */
 int cmpc_comm_gather_solution(cmpc_handle h, int root, double *X, double *U, int32_t *scp_status,
                               int32_t *iterations, int32_t *qp_status);
 

@@ -5,7 +5,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, 'centroidal-mpc_amd')]
 import numpy as np
 from cmpc._lib import Solver
 from cmpc.synth import make_batch
-for cfg, N, B in (('trot', 20, 64), ('trot', 100, 256), ('bound', 20, 64), ('pace', 40, 64))):
+for cfg, N, B in (('trot', 20, 64), ('trot', 100, 256), ('bound', 20, 64), ('pace', 40, 64)):
     pb = make_batch(cfg, N, B)
     for prec in ('fp32',):
         s = Solver(pb.robot, N, B, prec)

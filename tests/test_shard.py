@@ -92,3 +92,38 @@ def test_bench_gpus_flag_spawns_one_process_per_gpu(tmp_path):
                        timeout=300)
     assert r.returncode != 0
     assert '"n_gpus"' not in r.stdout
+
+
+def test_bench_multirank_orchestration_on_cpu(tmp_path):
+    """bench.py's multi-rank path end to end in two processes (tests/bench_stub.py: CPU stubs for the
+    device Solver and a socket-based RcclComm): each rank uploads its contiguous slice of the
+    global batch, the timed region sits between two barriers and takes the max over ranks, the
+    weak-scaling leg runs, the accepted solutions are gathered to rank 0 in global order, and only
+    rank 0 prints the one JSON line."""
+    import json
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env['HIP_VISIBLE_DEVICES'] = ''
+    B, N = 1024, 10
+    rc = spawn_local(2, [os.path.join(root, 'tests', 'bench_stub.py'), str(tmp_path), '--gpus', '2', '--steps', '3',
+                         '--warmup', '1', '--batch', str(B), '--N', str(N), '--no-cpu-baseline'], env=env, timeout=600)
+    assert rc == 0
+    lines0 = [l for l in (tmp_path / 'rank0.txt').read_text().splitlines() if l.strip()]
+    lines1 = [l for l in (tmp_path / 'rank1.txt').read_text().splitlines() if l.strip()]
+    assert len(lines0) == 1 and lines1 == []
+    out = json.loads(lines0[0])
+    assert out['n_gpus'] == 2 and out['scaling'] == 'strong' and out['steps'] == 3
+    assert out['config']['global_batch'] == B and out['config']['batch_per_gpu'] == B // 2
+    assert out['value'] == pytest.approx(B * 3 / (out['ms_per_step'] * 3 / 1e3))
+    assert out['weak_scaling']['global_batch'] == 2 * B and out['weak_scaling']['per_gpu'] == B
+    assert out['gather_ms'] >= 0 and out['early_exit']['scp_iterations'] == B
+    # the gather holds both slices in the global problem order
+    g = np.load(tmp_path / 'gather.npz')
+    full = make_batch('trot', N, B, seed_offset=0)
+    assert g['X'].shape == (B, N + 1, 9)
+    np.testing.assert_array_equal(g['X'][:, 0, :], full.Xbar[:, 0, :])
+    # barriers: 1 (timed, start) + 1 (clock) per timed leg x 2 legs, the gather's barrier, and the
+    # early-exit barrier + clock: the same count on both ranks
+    c0 = (tmp_path / 'calls0.txt').read_text().split()
+    c1 = (tmp_path / 'calls1.txt').read_text().split()
+    assert c0 == c1 and int(c0[1]) == 1 and int(c0[0]) >= 6
