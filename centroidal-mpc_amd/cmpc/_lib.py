@@ -78,7 +78,8 @@ EXPORTS = ['cmpc_create', 'cmpc_destroy', 'cmpc_last_error', 'cmpc_version', 'cm
            'cmpc_upload_states', 'cmpc_get_contact_plans', 'cmpc_get_warm_start', 'cmpc_get_qp_info',
            'cmpc_comm_get_unique_id', 'cmpc_comm_init', 'cmpc_comm_destroy', 'cmpc_comm_bcast_params',
            'cmpc_comm_allreduce_max', 'cmpc_comm_gather_solution', 'cmpc_load_qp', 'cmpc_get_iteration_history',
-           'cmpc_get_accepted']
+           'cmpc_get_accepted', 'cmpc_host_register', 'cmpc_host_unregister',
+           'cmpc_prefetch_ks']
 SCP_MODE = {'reference': 0, 'gusto': 1}
 
 _lib = None
@@ -143,6 +144,9 @@ def load():
         'cmpc_load_qp': (i32, [h, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
         'cmpc_get_iteration_history': (i32, [h, i32, vp, vp]),
         'cmpc_get_accepted': (i32, [h, i32, vp, vp, vp, vp]),
+        'cmpc_host_register': (i32, [h, vp, ctypes.c_size_t]),
+        'cmpc_host_unregister': (i32, [h, vp]),
+        'cmpc_prefetch_ks': (i32, [h, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -215,6 +219,9 @@ class Solver:
 
     def close(self):
         if getattr(self, 'h', None) is not None and self.h.value:
+            for a in (getattr(self, '_pinned', None) or {}).values():
+                self.lib.cmpc_host_unregister(self.h, a.ctypes.data_as(ctypes.c_void_p))
+            self._pinned = None
             self.lib.cmpc_destroy(self.h)
             self.h = None
 
@@ -412,15 +419,45 @@ class Solver:
         self._chk(self.lib.cmpc_get_qp_info(self.h, _ptr(merit), _ptr(nref)), 'cmpc_get_qp_info')
         return merit, nref
 
-    def solution(self):
+    def solution(self, pinned=False, with_ks=True):
+        """Accepted X, U (and with_ks K, Sigma) plus the per-problem SCP state.  pinned=True writes
+        into output arrays kept by this Solver and page-locked once (cmpc_host_register), so the
+        copies run by DMA at full link rate and no fresh pages are faulted in per call; the arrays
+        are then overwritten by the next pinned call (copy what must be kept)."""
         B, N = self.B, self.N
-        out = dict(X=np.zeros((B, N + 1, 9)), U=np.zeros((B, N, 12)), K=np.zeros((B, N, 12, 9)),
-                   Sigma=np.zeros((B, N + 1, 9, 9)), n_accepted=np.zeros(B, np.int32),
-                   iterations=np.zeros(B, np.int32), status=np.zeros(B, np.int32), weight=np.zeros(B),
-                   radius=np.zeros(B))
+        shapes = dict(X=(B, N + 1, 9), U=(B, N, 12), K=(B, N, 12, 9), Sigma=(B, N + 1, 9, 9))
+        if pinned:
+            bufs = self._pinned_outputs()
+            out = {k: bufs[k][:int(np.prod(v))].reshape(v) for k, v in shapes.items()}
+        else:
+            out = {k: np.zeros(v) for k, v in shapes.items()}
+        if not with_ks:
+            out['K'] = out['Sigma'] = None
+        out.update(n_accepted=np.zeros(B, np.int32), iterations=np.zeros(B, np.int32), status=np.zeros(B, np.int32),
+                   weight=np.zeros(B), radius=np.zeros(B))
         keys = ('X', 'U', 'K', 'Sigma', 'n_accepted', 'iterations', 'status', 'weight', 'radius')
         self._chk(self.lib.cmpc_get_solution(self.h, *[_ptr(out[k]) for k in keys]), 'cmpc_get_solution')
         return out
+
+    def prefetch_ks(self):
+        """Reference mode: stream the next solve's accepted K and Sigma into this Solver's pinned
+        output arrays while it runs (cmpc_prefetch_ks); solution(pinned=True) then only waits."""
+        bufs = self._pinned_outputs()
+        self._chk(self.lib.cmpc_prefetch_ks(self.h, _ptr(bufs['K']), _ptr(bufs['Sigma'])), 'cmpc_prefetch_ks')
+
+    def _pinned_outputs(self):
+        """Flat fp64 output arrays for max_batch problems, page-locked once per Solver."""
+        if getattr(self, '_pinned', None) is None:
+            Bm, N = self.max_batch, self.N
+            sizes = dict(X=Bm * (N + 1) * 9, U=Bm * N * 12, K=Bm * N * 12 * 9, Sigma=Bm * (N + 1) * 81)
+            self._pinned = {}
+            for k, n in sizes.items():
+                a = np.empty(n)
+                a.fill(0.0)   # fault the pages in once
+                self._chk(self.lib.cmpc_host_register(self.h, a.ctypes.data_as(ctypes.c_void_p), a.nbytes),
+                          'cmpc_host_register')
+                self._pinned[k] = a
+        return self._pinned
 
     def iteration_log(self):
         B = self.B

@@ -30,6 +30,7 @@ template <typename T, int R> __global__ void k_accept(DevBuf<T>, int);
 template <typename T> __global__ void k_keep_accepted(DevBuf<T>);
 template <typename T> __global__ void k_knot_major(const T *, size_t, size_t, size_t, int, double *);
 template <typename T, int R> __global__ void k_rollout(DevBuf<T>, const T *, const T *, T *);
+__global__ void k_widen(const float *, size_t, double *);
 size_t ipm_workspace_elems(int N, int robot);
 }  // namespace cmpc
 
@@ -336,6 +337,11 @@ void ensure_dense(cmpc_handle h) {
 // point, new contact plans change it), they are copied to Kacc / Sacc once and copied per accept
 // from then on.
 void materialize_accepted_ks(cmpc_handle h) {
+    if (h->pf_armed || h->pfK_issued || h->pfS_issued) {   // a prefetch serves live arrays only
+        if (h->pfK_issued || h->pfS_issued) HIPCHK(hipStreamSynchronize(h->copy));
+        h->pf_armed = h->pfK_issued = h->pfS_issued = false;
+        h->pf_K = h->pf_S = nullptr;
+    }
     if (!h->ks_live) return;
     settle_all(h);   // Sigma of a deferred scan first
     if (h->B > 0) {
@@ -400,8 +406,69 @@ void ensure_history(cmpc_handle h) {
     }
 }
 
+// ---- K / Sigma prefetch (cmpc_prefetch_ks).  In reference mode the linearization point never
+// moves (Q1): K is final once the first iteration's linearization ran and Sigma once its scan ran,
+// and the accepted K / Sigma are those arrays.  The copies to the caller's page-locked buffers
+// then run on the copy stream's DMA while the QP runs (K) or while the accept step and the
+// caller's own getters run (Sigma).
+void pf_disarm(cmpc_handle h) {
+    if (h->pfK_issued || h->pfS_issued) HIPCHK(hipStreamSynchronize(h->copy));
+    h->pf_armed = h->pfK_issued = h->pfS_issued = false;
+    h->pf_K = h->pf_S = nullptr;
+}
+
+double *pf_staging(cmpc_handle h, size_t bytes) {
+    if (bytes > h->pf_stage_bytes) {
+        HIPCHK(hipStreamSynchronize(h->copy));
+        h->regrow(h->pf_stage, bytes);
+        h->pf_stage_bytes = bytes;
+    }
+    return (double *)h->pf_stage;
+}
+
+// after phase 0 on the main stream: K (transposed / widened on the main stream, ~40 us) to the host
+void pf_issue_K(cmpc_handle h) {
+    if (!h->pf_armed || h->pfK_issued || !h->pf_K || h->scp_mode != CMPC_SCP_MODE_REFERENCE || !h->ks_live) return;
+    const size_t B = h->B, N = h->N, LS = (size_t)h->max_batch * N, nK = B * N * NU * 9;
+    double *stg = pf_staging(h, (nK + (h->prec == CMPC_PREC_F32 ? B * (N + 1) * 81 : 0)) * sizeof(double));
+    const dim3 grid((unsigned)((B * N + 31) / 32), (unsigned)((NU * 9 + 31) / 32));
+    if (h->prec == CMPC_PREC_F32)
+        hipLaunchKernelGGL((k_knot_major<float>), grid, dim3(256), 0, h->stream, (const float *)h->K, LS, (size_t)0, B * N,
+                           (int)(NU * 9), stg);
+    else
+        hipLaunchKernelGGL((k_knot_major<double>), grid, dim3(256), 0, h->stream, (const double *)h->K, LS, (size_t)0,
+                           B * N, (int)(NU * 9), stg);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(h->ev_pf_src, h->stream));
+    HIPCHK(hipStreamWaitEvent(h->copy, h->ev_pf_src, 0));
+    HIPCHK(hipMemcpyAsync(h->pf_K, stg, nK * sizeof(double), hipMemcpyDeviceToHost, h->copy));
+    HIPCHK(hipEventRecord(h->ev_pfK, h->copy));
+    h->pfK_issued = true;
+}
+
+// after the QP on the main stream (the covariance scans have joined it there): Sigma to the host
+void pf_issue_S(cmpc_handle h) {
+    if (!h->pf_armed || h->pfS_issued || !h->pf_S || h->scp_mode != CMPC_SCP_MODE_REFERENCE || !h->ks_live) return;
+    if (h->scan_deferred || h->scan_pending) return;   // not yet joined (phase-by-phase callers)
+    const size_t B = h->B, N = h->N, nS = B * (N + 1) * 81, nK = B * N * NU * 9;
+    const void *src = h->Sig;
+    if (h->prec == CMPC_PREC_F32) {
+        double *stg = pf_staging(h, (nK + nS) * sizeof(double)) + nK;
+        hipLaunchKernelGGL(k_widen, dim3((unsigned)std::min<size_t>((nS + 255) / 256, 4096)), dim3(256), 0, h->stream,
+                           (const float *)h->Sig, nS, stg);
+        HIPCHK(hipGetLastError());
+        src = stg;
+    }
+    HIPCHK(hipEventRecord(h->ev_pf_src, h->stream));
+    HIPCHK(hipStreamWaitEvent(h->copy, h->ev_pf_src, 0));
+    HIPCHK(hipMemcpyAsync(h->pf_S, src, nS * sizeof(double), hipMemcpyDeviceToHost, h->copy));
+    HIPCHK(hipEventRecord(h->ev_pfS, h->copy));
+    h->pfS_issued = true;
+}
+
 void reset_scp(cmpc_handle h, const int32_t *class_id) {
-    settle_all(h);   // a scan still pending reads the previous batch's arrays
+    settle_all(h);
+    pf_disarm(h);   // a prefetch belongs to one solve of one upload   // a scan still pending reads the previous batch's arrays
     h->ks_live = h->scp_mode == CMPC_SCP_MODE_REFERENCE;
     h->lin_lane_done = false;   // new inputs: nothing to recompute densely until the next linearization
     std::vector<ScpState> st(h->B);
@@ -487,6 +554,10 @@ int cmpc_create(cmpc_handle *out, int device, int robot, int N, int max_batch, i
         HIPCHK(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, prio_low));
         HIPCHK(hipEventCreateWithFlags(&h->ev_asm, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&h->ev_scan, hipEventDisableTiming));
+        HIPCHK(hipStreamCreateWithFlags(&h->copy, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&h->ev_pf_src, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&h->ev_pfK, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&h->ev_pfS, hipEventDisableTiming));
         h->scan_ctr = h->dalloc(16);
         HIPCHK(hipDeviceGetAttribute(&h->n_cu, hipDeviceAttributeMultiprocessorCount, device));
         for (auto &e : h->ev) HIPCHK(hipEventCreate(&e));
@@ -541,6 +612,7 @@ int cmpc_destroy(cmpc_handle h) {
     if (!h) return 0;
     (void)hipSetDevice(h->device);
     if (h->side) (void)hipStreamSynchronize(h->side);
+    if (h->copy) (void)hipStreamSynchronize(h->copy);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->comm && h->comm_free) h->comm_free(h->comm);
     for (void *p : h->allocs) (void)hipFree(p);
@@ -549,6 +621,9 @@ int cmpc_destroy(cmpc_handle h) {
         if (e) (void)hipEventDestroy(e);
     for (auto &a : h->ev_pool)
         for (auto &e : a) (void)hipEventDestroy(e);
+    for (hipEvent_t e : {h->ev_pf_src, h->ev_pfK, h->ev_pfS})
+        if (e) (void)hipEventDestroy(e);
+    if (h->copy) (void)hipStreamDestroy(h->copy);
     if (h->ev_asm) (void)hipEventDestroy(h->ev_asm);
     if (h->ev_scan) (void)hipEventDestroy(h->ev_scan);
     if (h->side) (void)hipStreamDestroy(h->side);
@@ -800,10 +875,12 @@ int cmpc_scp_iterate(cmpc_handle h, int fixed_iters) {
         }
         HIPCHK(hipEventRecord(ev[0], h->stream));
         phase(h, 0, oa, true);   // the covariance scan may run beside the QP (launch_phase)
+        pf_issue_K(h);
         HIPCHK(hipEventRecord(ev[1], h->stream));
         phase(h, 1, oa);
         HIPCHK(hipEventRecord(ev[2], h->stream));
         phase(h, 2, oa);
+        pf_issue_S(h);
         HIPCHK(hipEventRecord(ev[3], h->stream));
         phase(h, 3, oa);
         HIPCHK(hipEventRecord(ev[4], h->stream));
@@ -1030,15 +1107,60 @@ int cmpc_get_solution(cmpc_handle h, double *X, double *U, double *K, double *Si
                       int32_t *iterations, int32_t *scp_status, double *weight, double *radius) {
     return guard(h, [&] {
         settle_all(h);
-        const size_t B = h->B, N = h->N, K1 = N + 1;
-        auto dl = [&](double *dst, void *src, size_t n) {
-            if (h->prec == CMPC_PREC_F64) from_dev<double>(h, dst, src, n); else from_dev<float>(h, dst, src, n);
+        const size_t B = h->B, N = h->N, K1 = N + 1, LS = (size_t)h->max_batch * N;
+        // Everything is brought into the host layouts on the device first (fp64; K transposed to
+        // knot-major; fp32 handles widened), then one batch of asynchronous copies and one
+        // synchronization.  Destinations the caller pinned (cmpc_host_register) are written by DMA
+        // at full link rate; pageable ones through the runtime's staging.  NULL skips an array.
+        const size_t nX = B * K1 * 9, nU = B * N * NU, nK = B * N * NU * 9, nS = B * K1 * 81;
+        const void *Ssrc = h->ks_live ? h->Sig : h->Sacc, *Ksrc = h->ks_live ? h->K : h->Kacc;
+        // arrays the solve already streamed into these same buffers (cmpc_prefetch_ks): only wait
+        bool waitK = false, waitS = false;
+        if (K && h->pfK_issued && K == h->pf_K) { waitK = true; K = nullptr; }
+        if (Sigma && h->pfS_issued && Sigma == h->pf_S) { waitS = true; Sigma = nullptr; }
+        const bool f32 = h->prec == CMPC_PREC_F32;
+        size_t need_el = K ? nK : 0;
+        if (f32) need_el += (X ? nX : 0) + (U ? nU : 0) + (Sigma ? nS : 0);
+        double *stg = need_el ? (double *)h->scratch_bytes_at_least(need_el * sizeof(double)) : nullptr;
+        const double *srcX = (const double *)h->Xacc, *srcU = (const double *)h->Uacc, *srcS = (const double *)Ssrc,
+                     *srcK = nullptr;
+        size_t off = 0;
+        auto widen = [&](const void *src, size_t n) {
+            double *dst = stg + off;
+            off += n;
+            hipLaunchKernelGGL(k_widen, dim3((unsigned)std::min<size_t>((n + 255) / 256, 4096)), dim3(256), 0, h->stream,
+                               (const float *)src, n, dst);
+            return (const double *)dst;
         };
-        dl(X, h->Xacc, B * K1 * 9);
-        dl(U, h->Uacc, B * N * NU);
-        dl_knots(h, K, h->ks_live ? h->K : h->Kacc, 0, B * N, NU * 9);
-        dl(Sigma, h->ks_live ? h->Sig : h->Sacc, B * K1 * 81);
-        auto st = get_scp(h);
+        if (K) {
+            const dim3 grid((unsigned)((B * N + 31) / 32), (unsigned)((NU * 9 + 31) / 32));
+            if (f32)
+                hipLaunchKernelGGL((k_knot_major<float>), grid, dim3(256), 0, h->stream, (const float *)Ksrc, LS, (size_t)0,
+                                   B * N, (int)(NU * 9), stg);
+            else
+                hipLaunchKernelGGL((k_knot_major<double>), grid, dim3(256), 0, h->stream, (const double *)Ksrc, LS, (size_t)0,
+                                   B * N, (int)(NU * 9), stg);
+            srcK = stg;
+            off = nK;
+        }
+        if (f32) {
+            if (X) srcX = widen(h->Xacc, nX);
+            if (U) srcU = widen(h->Uacc, nU);
+            if (Sigma) srcS = widen(Ssrc, nS);
+        }
+        HIPCHK(hipGetLastError());
+        auto out = [&](double *dst, const double *src, size_t n) {
+            if (dst && n) HIPCHK(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+        };
+        out(K, srcK, nK);
+        out(X, srcX, nX);
+        out(U, srcU, nU);
+        out(Sigma, srcS, nS);
+        std::vector<ScpState> st(B);
+        HIPCHK(hipMemcpyAsync(st.data(), h->scp, B * sizeof(ScpState), hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+        if (waitK) HIPCHK(hipEventSynchronize(h->ev_pfK));
+        if (waitS) HIPCHK(hipEventSynchronize(h->ev_pfS));
         for (size_t b = 0; b < B; ++b) {
             if (n_accepted) n_accepted[b] = st[b].n_accepted;
             if (iterations) iterations[b] = st[b].iter;
@@ -1046,6 +1168,35 @@ int cmpc_get_solution(cmpc_handle h, double *X, double *U, double *K, double *Si
             if (weight) weight[b] = st[b].weight;
             if (radius) radius[b] = st[b].radius;
         }
+    });
+}
+
+int cmpc_prefetch_ks(cmpc_handle h, double *K, double *Sigma) {
+    return guard(h, [&] {
+        need(h->B > 0, "no problems uploaded");
+        need(h->scp_mode == CMPC_SCP_MODE_REFERENCE && h->ks_live,
+             "prefetch serves reference mode's live K / Sigma (upload first; not in GuSTO mode)");
+        pf_disarm(h);
+        h->pf_K = K;
+        h->pf_S = Sigma;
+        h->pf_armed = K || Sigma;
+        // staging sized now, not inside the solve
+        const size_t B = h->B, N = h->N;
+        pf_staging(h, (B * N * NU * 9 + (h->prec == CMPC_PREC_F32 ? B * (N + 1) * 81 : 0)) * sizeof(double));
+    });
+}
+
+int cmpc_host_register(cmpc_handle h, void *ptr, size_t bytes) {
+    return guard(h, [&] {
+        need(ptr != nullptr && bytes > 0, "invalid host range");
+        HIPCHK(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+    });
+}
+
+int cmpc_host_unregister(cmpc_handle h, void *ptr) {
+    return guard(h, [&] {
+        need(ptr != nullptr, "invalid host pointer");
+        HIPCHK(hipHostUnregister(ptr));
     });
 }
 

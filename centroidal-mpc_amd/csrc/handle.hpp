@@ -78,6 +78,14 @@ struct cmpc_handle_s {
     // iterations per problem; the K / Sigma slots exist only once GuSTO mode ran
     void *hlog = nullptr, *hX = nullptr, *hU = nullptr, *hK = nullptr, *hS = nullptr;
     int log_cap = 0, hist_cap = 0, hks_cap = 0;
+    // K / Sigma prefetch of the reference-mode loop (cmpc_prefetch_ks): pinned host targets, a copy
+    // stream, the staging of the transposed (or widened) arrays, and what has been issued
+    double *pf_K = nullptr, *pf_S = nullptr;
+    hipStream_t copy = nullptr;
+    hipEvent_t ev_pf_src = nullptr, ev_pfK = nullptr, ev_pfS = nullptr;
+    void *pf_stage = nullptr;
+    size_t pf_stage_bytes = 0;
+    bool pf_armed = false, pfK_issued = false, pfS_issued = false;
     // grow-only device scratch of the host getters (knot-major staging copies)
     void *scratch = nullptr;
     size_t scratch_bytes = 0;

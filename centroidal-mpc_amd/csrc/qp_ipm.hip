@@ -408,15 +408,10 @@ template <int n, typename T, typename P> __device__ __forceinline__ void stv(P p
 // then move above the stores, so every result row is stored as soon as it is formed and the
 // phase never holds the whole knot in registers (holding it serialized the loads of late rows
 // behind one memory round trip each).
-// Mixed precision for the fp32 kernels: the residuals are formed in fp64 from the fp32 iterate
-// and records (Acc<float> = double), then rounded once on store.  In fp32 the dual rows of the
-// states sum terms of ~1e3-1e5 (W_x x, q = -W_x xbar, E' nu) that cancel to ~1e-2: fp32 sums left a
-// floor of ~7e-3 on Solo12 trot, above the 1e-6 relative tolerance, so the iteration ran on until
-// mu underflowed (status -10, tests/golden trot_f32).  With exact residuals the Newton steps,
-// still fp32, refine the iterate down to what fp32 can represent, as in mixed-precision iterative
-// refinement.  fp64: Acc<double> = double, the same code as before.
+// Accumulation type of the residuals (kept as a hook: fp64 residuals for the fp32 kernels were
+// tried, Acc<float> = double, and cost C3's QP 15% (0.73 -> 0.84 ms) without changing its exits;
+// the fp32 floor on Solo12 trot came from the dual scale, see the multiplier term below).
 template <typename T> struct Acc { using type = T; };
-template <> struct Acc<float> { using type = double; };
 
 template <typename T, int ROBOT>
 __device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<T, ROBOT> &nm, const T *__restrict__ stp,

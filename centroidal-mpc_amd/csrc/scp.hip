@@ -403,6 +403,11 @@ template __global__ void k_rollout<double, 1>(DevBuf<double>, const double *, co
 template __global__ void k_rollout<float, 0>(DevBuf<float>, const float *, const float *, float *);
 template __global__ void k_rollout<float, 1>(DevBuf<float>, const float *, const float *, float *);
 
+// fp32 handles: widen n values into the fp64 staging buffer of a getter (coalesced, grid-stride)
+__global__ void __launch_bounds__(256) k_widen(const float *src, size_t n, double *dst) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) dst[i] = double(src[i]);
+}
+
 template __global__ void k_knot_major<double>(const double *, size_t, size_t, size_t, int, double *);
 template __global__ void k_knot_major<float>(const float *, size_t, size_t, size_t, int, double *);
 template __global__ void k_keep_accepted<double>(DevBuf<double>);

@@ -36,6 +36,7 @@
 #ifndef CMPC_H
 #define CMPC_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -225,6 +226,19 @@ int cmpc_get_qp_info(cmpc_handle h, double *merit, int32_t *n_refine);
  * arrays).  GuSTO mode and new contact plans copy them per accept. */
 int cmpc_get_solution(cmpc_handle h, double *X, double *U, double *K, double *Sigma, int32_t *n_accepted,
                       int32_t *iterations, int32_t *scp_status, double *weight, double *radius);
+/* Page-lock a caller's host range (hipHostRegister) so getters write it by DMA at full link rate
+ * (cmpc_get_solution: X, U, K, Sigma of a 1024-problem N=100 batch are 172 MB); unregister
+ * before freeing it.  Optional: pageable buffers work, through the runtime's staging copies. */
+int cmpc_host_register(cmpc_handle h, void *ptr, size_t bytes);
+/* Reference mode: stream the accepted K (B,N,nu,9) and Sigma (B,N+1,9,9) of the next solve into
+ * these page-locked host buffers (NULL skips) while it runs.  The linearization point never moves
+ * (quirk Q1), so K is final after the first iteration's linearization and Sigma after its
+ * covariance scan: the copies run on a copy stream's DMA behind the QP.  A following
+ * cmpc_get_solution given the same pointers only waits for them.  Armed until the next upload
+ * (or a mode / parameter / plan change); only problems with n_accepted > 0 have accepted K / Sigma
+ * (the others get the linearization's, as cmpc_get_solution returns them). */
+int cmpc_prefetch_ks(cmpc_handle h, double *K, double *Sigma);
+int cmpc_host_unregister(cmpc_handle h, void *ptr);
 /* The last iteration of each problem (B entries each; NULL skips). */
 int cmpc_get_iteration_log(cmpc_handle h, double *tr_norm, double *rho, int32_t *qp_status,
                            int32_t *qp_iters, int32_t *decision);

@@ -77,12 +77,15 @@ class StubSolver:
         self.scp_iterate()
         return 1
 
-    def solution(self):
+    def solution(self, pinned=False, with_ks=True):
         B, N = self.B, self.N
         X = np.broadcast_to(self.first.Xbar[:, :, :], (B, N + 1, 9)).copy()
         return dict(X=X, U=np.zeros((B, N, 12)), K=np.zeros((B, N, 12, 9)), Sigma=np.zeros((B, N + 1, 9, 9)),
                     n_accepted=np.ones(B, np.int32), iterations=np.ones(B, np.int32),
                     status=np.ones(B, np.int32), weight=np.zeros(B), radius=np.zeros(B))
+
+    def prefetch_ks(self):
+        pass
 
     def close(self):
         pass
