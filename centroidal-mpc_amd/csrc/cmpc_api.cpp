@@ -99,8 +99,11 @@ template <typename T> DevParams<T> conv_params(const cmpc_params &p, int nw) {
 // QP waves per problem: the setting, or (0) two when the batch at two waves per problem still runs
 // in one round on the device (one wave per SIMD at ~500 registers per lane) and the horizon needs
 // more than one pass of 64 knots
+// Four waves (schur_pt.hpp: the Schur recurrence as four chains) when every problem still gets a
+// CU of its own and the horizon gives each chain a few blocks.
 int qp_waves(cmpc_handle h) {
-    if (h->qs.waves_per_problem > 0) return h->qs.waves_per_problem;
+    if (h->qs.waves_per_problem > 0) return h->qs.waves_per_problem == 4 && h->N < 16 ? 2 : h->qs.waves_per_problem;
+    if (h->N >= 40 && (long)h->B <= (long)h->n_cu) return 4;
     return (h->N + 1 > 64 && 2L * h->B <= 4L * h->n_cu) ? 2 : 1;
 }
 
@@ -133,7 +136,7 @@ template <typename T, int R> void launch_scan(cmpc_handle h, hipStream_t s, int 
 // C4 59.5k -> 60.5k; same-box A/B, profiles/r02_scan_overlap_ab.txt).
 bool scan_beside_qp(cmpc_handle h) {
     const int w = qp_waves(h);
-    return w == 2 || (long)h->B * w < 4L * h->n_cu;
+    return w >= 2 || (long)h->B * w < 4L * h->n_cu;
 }
 
 bool any_stochastic(cmpc_handle h) {
@@ -208,8 +211,9 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
         const int nt = 64 * qp_waves(h);
         const T eta = T(qp_step_fraction(h));
         const size_t lds = ipm_lds_bytes(h->N, (int)sizeof(T), nt);
-        const void *fn = nt == 128 ? reinterpret_cast<const void *>(&k_qp_ipm<T, R, 128>)
-                                   : reinterpret_cast<const void *>(&k_qp_ipm<T, R, 64>);
+        const void *fn = nt == 256   ? reinterpret_cast<const void *>(&k_qp_ipm<T, R, 256>)
+                         : nt == 128 ? reinterpret_cast<const void *>(&k_qp_ipm<T, R, 128>)
+                                     : reinterpret_cast<const void *>(&k_qp_ipm<T, R, 64>);
         HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         if (h->scan_deferred) {   // the scans run in the QP's workgroups (one-wave kernel only)
             need(nt == 64, "internal: QP scan jobs need the one-wave kernel");
@@ -217,7 +221,11 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
             d.scan_ctr = (unsigned *)h->scan_ctr;
             h->scan_deferred = false;
         }
-        if (nt == 128)
+        if (nt == 256)
+            hipLaunchKernelGGL((k_qp_ipm<T, R, 256>), dim3(B), dim3(256), lds, h->stream, d, only_active,
+                               h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), eta,
+                               T(h->qs.init_floor_s), T(h->qs.init_floor_l));
+        else if (nt == 128)
             hipLaunchKernelGGL((k_qp_ipm<T, R, 128>), dim3(B), dim3(128), lds, h->stream, d, only_active,
                                h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), eta,
                                T(h->qs.init_floor_s), T(h->qs.init_floor_l));
@@ -635,8 +643,9 @@ int cmpc_destroy(cmpc_handle h) {
 int cmpc_set_qp_settings(cmpc_handle h, const cmpc_qp_settings *s) {
     return guard(h, [&] {
         need(s && s->max_iter > 0 && s->step_fraction >= 0 && s->step_fraction < 1 && s->init_floor_s >= 0 &&
-                 s->init_floor_l >= 0 && (s->init_floor_s > 0) == (s->init_floor_l > 0) && s->waves_per_problem >= 0 &&
-                 s->waves_per_problem <= 2, "invalid QP settings");
+                 s->init_floor_l >= 0 && (s->init_floor_s > 0) == (s->init_floor_l > 0) &&
+                 (s->waves_per_problem == 0 || s->waves_per_problem == 1 || s->waves_per_problem == 2 ||
+                  s->waves_per_problem == 4), "invalid QP settings");
         h->qs = *s;
     });
 }

@@ -56,9 +56,11 @@ template <int ROBOT> struct Ws {
         wt = wx + 9, wu = wt + 1, dx = wu + NU, dt = dx + 9, du = dt + 1, ds = du + NU, dl = ds + NI,
         dsa = dl + NI, dla = dsa + NI, rh = dla + NI, dn0 = rh + NI, NF = dn0 + 9
     };
-    // Schur blocks (block-major 9x9): S_jj -> I_j, and S_{j,j+1} -> X_{j+1} / Y_j (tw_factor_ends)
-    static constexpr size_t Sd = (size_t)NF * KPC, So = Sd + (size_t)NBMAX * 81;
-    static constexpr size_t total = (So + (size_t)NBMAX * 81 + 7) & ~size_t(7);
+    // Schur blocks (block-major 9x9): S_jj -> I_j, and S_{j,j+1} -> X_{j+1} / Y_j (tw_factor_ends);
+    // four-wave workgroups also the fill factors H_j and the separator scratch (schur_pt.hpp)
+    static constexpr size_t Sd = (size_t)NF * KPC, So = Sd + (size_t)NBMAX * 81, Sh = So + (size_t)NBMAX * 81,
+                            Sx = Sh + (size_t)NBMAX * 81;
+    static constexpr size_t total = (Sx + (size_t)16 * 81 + 7) & ~size_t(7);
 };
 
 template <typename T> __device__ __forceinline__ T rcp_nr(T p) {
@@ -171,6 +173,9 @@ template <typename T, int ROBOT> struct Ctx {
     // multi-wave workgroups: w_x of knot k (k >= 1) parked here by phase_w and added to Schur block
     // k after the phase's barrier (add_wx), since block k's other terms come from another wave
     LdsT<T> *wxs = nullptr;
+    T *Sh = nullptr, *Sx = nullptr;   // four-wave workgroups: fill factors, separator scratch (schur_pt.hpp)
+    int sp[3] = {0, 0, 0};            // four-wave workgroups: separator blocks
+    LdsT<T> *sbv = nullptr, *hy = nullptr;   // separator right-hand-side terms, fill products
     __device__ unsigned cmask(int k) const { return cm ? unsigned(cm[k]) : cmask_mem(k); }
     __device__ unsigned cmask_mem(int k) const {
         if (k >= N) return 0u;
@@ -1404,6 +1409,8 @@ __device__ void tw_solve_back(const T *Xs, int NB, int m, LdsT<T> *vb, LdsT<T> *
     wave_sync();
 }
 
+#include "schur_pt.hpp"
+
 // r_hat = r_i - r_c / lambda for the rows of knot k.  corr 0 (predictor): r_c = s lambda; 1
 // (corrector): r_c = s lambda + ds_aff dlambda_aff - sigma mu; 2 (refinement): r_c = the dsa
 // field, which then holds the complementarity residual of the corrector direction (phase_lres)
@@ -1938,6 +1945,45 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_init_shift(con
     }
 }
 
+// Forward elimination + separator / meeting-block solve of the right-hand side in vb, and the back
+// substitution, with the factors of this Newton step: the two-ended recurrence (one or two waves)
+// or the four chains of schur_pt.hpp (four waves).  Barriers included.
+template <typename T, int NTT, typename CT>
+__device__ __forceinline__ void schur_forward(const CT &C, int NB, int NBm, LdsT<T> *ring, LdsT<T> *shl) {
+    const int tid = threadIdx.x;
+    if constexpr (NTT >= 256) {
+        pt_solve_elim<T>(C.So, NB, C.sp, C.vb, ring, C.sbv);
+        __syncthreads();
+        pt_fill_rhs<T, NTT>(C.Sh, C.sp, C.vb, C.hy);
+        __syncthreads();
+        if (tid < 64) {
+            pt_fill_sum<T>(C.sp, C.hy, C.sbv);
+            pt_reduced<T>(C.Sd, C.Sx, C.sp, shl, C.vb, C.sbv, false);
+        }
+        __syncthreads();
+    } else {
+        if (tid < 64) tw_solve_elim<T>(C.So, NB, NBm, C.vb, ring);
+        __syncthreads();
+        if (tid < 64) tw_solve_meet<T>(C.Sd, C.So, NB, NBm, C.vb, shl);
+        __syncthreads();
+    }
+}
+template <typename T, int NTT, typename CT>
+__device__ __forceinline__ void schur_backward(const CT &C, int NB, int NBm, LdsT<T> *ring) {
+    const int tid = threadIdx.x;
+    if constexpr (NTT >= 256) {
+        pt_solve_local<T, NTT>(C.Sd, C.Sh, NB, C.sp, C.vb);
+        __syncthreads();
+        pt_solve_back<T>(C.So, NB, C.sp, C.vb, ring);
+        __syncthreads();
+    } else {
+        tw_solve_local<T, NTT>(C.Sd, NB, NBm, C.vb);
+        __syncthreads();
+        if (tid < 64) tw_solve_back<T>(C.So, NB, NBm, C.vb, ring);
+        __syncthreads();
+    }
+}
+
 // One step of iterative refinement of the corrector direction; returns the new step bound.
 // (Inlined: as an outlined call, the registers live across it were reloaded from scratch all over
 // the Newton step.)
@@ -1953,14 +1999,8 @@ __device__ __forceinline__ T refine_direction(const Ctx<T, ROBOT> &C, T sigma_mu
         add_wx<T, NTT>(C.vb, C.wxs, C.N);
         __syncthreads();
     }
-    if (tid < 64) tw_solve_elim<T>(C.So, NB, NBm, C.vb, ring);
-    __syncthreads();
-    if (tid < 64) tw_solve_meet<T>(C.Sd, C.So, NB, NBm, C.vb, shl);
-    __syncthreads();
-    tw_solve_local<T, NTT>(C.Sd, NB, NBm, C.vb);
-    __syncthreads();
-    if (tid < 64) tw_solve_back<T>(C.So, NB, NBm, C.vb, ring);
-    __syncthreads();
+    schur_forward<T, NTT>(C, NB, NBm, ring, shl);
+    schur_backward<T, NTT>(C, NB, NBm, ring);
     T ar[1] = {T(1)};
     for (int k = tid; k < K1; k += NTT) ar[0] = fmin(ar[0], phase_dz_refine<T, ROBOT>(C, k));
     block_reduce<T, NTT, 1, 2>(ar, red);   // (its barriers order the dnu reads before the sum)
@@ -1979,7 +2019,8 @@ __global__ void __launch_bounds__(NTT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int o
     if (b >= d.B) return;
     if (only_active && !d.scp[b].active) return;
     __shared__ T red[8 * (NTT / 64)];
-    __shared__ T sh[2 * TW_SCRATCH];
+    __shared__ T sh[NTT >= 256 ? 4 * PT_SCRATCH : 2 * TW_SCRATCH];
+    __shared__ T sbv_s[NTT >= 256 ? 6 * 9 : 1];
     const int tid = threadIdx.x, N = d.N, K1 = N + 1, NB = N + 2, NBm = NB / 2;
     Ctx<T, ROBOT> C{N, nullptr, nullptr, nullptr, nullptr, T(0), T(0), nullptr, nullptr, nullptr, nullptr, T(0), T(0), T(0), nullptr};
     C.prm = d.params + d.class_id[b];
@@ -2009,10 +2050,20 @@ __global__ void __launch_bounds__(NTT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int o
     // dynamic LDS: the (N+2) x 9 Schur vector, then two block rings per wave for the sweeps
     LdsT<T> *shl = (LdsT<T> *)sh;
     C.vb = (LdsT<T> *)reinterpret_cast<T *>(dsmem);
-    LdsT<T> *ring = C.vb + ((NB * 9 + 7) & ~7) + ((tid & 63) >> 5) * SWEEP_LDS;   // per half-wave of wave 0
-    if (NTT > 64) C.wxs = C.vb + ((NB * 9 + 7) & ~7) + 2 * SWEEP_LDS;
+    // rings: one per half-wave of wave 0 (two-ended sweeps), one per wave (four-wave chains)
+    constexpr int NRING = NTT >= 256 ? 4 : 2;
+    const int vec = (NB * 9 + 7) & ~7;
+    LdsT<T> *ring = C.vb + vec + (NTT >= 256 ? (tid >> 6) : ((tid & 63) >> 5)) * SWEEP_LDS;
+    if (NTT > 64) C.wxs = C.vb + vec + NRING * SWEEP_LDS;
     C.Sd = C.ws + Ws<ROBOT>::Sd;
     C.So = C.ws + Ws<ROBOT>::So;
+    if (NTT >= 256) {
+        C.Sh = C.ws + Ws<ROBOT>::Sh;
+        C.Sx = C.ws + Ws<ROBOT>::Sx;
+        pt_seps<T>(NB, C.sp);
+        C.sbv = (LdsT<T> *)sbv_s;
+        C.hy = C.wxs + vec;
+    }
 #ifdef CMPC_STAMPS
     unsigned long long t_prev = __builtin_amdgcn_s_memtime(), t_acc[12] = {};
 #define STAMP(i)                                                               \
@@ -2111,14 +2162,34 @@ __global__ void __launch_bounds__(NTT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int o
 #else
         unsigned long long *fst = nullptr;
 #endif
-        if (NTT >= 128) {   // one end per wave (waves 0 and 1; any further waves wait at the barrier)
-            if (tid < 128) tw_factor_ends<T, 64>(C.Sd, C.So, NB, NBm, shl, C.vb, fst);
-        } else {            // one end per half of wave 0
-            tw_factor_ends<T, 32>(C.Sd, C.So, NB, NBm, shl, C.vb, fst);
+        if (NTT >= 256) {   // four chains and the separator system (schur_pt.hpp)
+#ifdef CMPC_STAMPS
+            const unsigned long long tc0 = __builtin_amdgcn_s_memtime();
+#endif
+            pt_factor_chains<T>(C.Sd, C.So, C.Sh, C.Sx, NB, C.sp, shl + (tid >> 6) * PT_SCRATCH, C.vb, C.sbv);
+#ifdef CMPC_STAMPS
+            const unsigned long long tc1 = __builtin_amdgcn_s_memtime();
+#endif
+            __syncthreads();
+#ifdef CMPC_STAMPS
+            const unsigned long long tc2 = __builtin_amdgcn_s_memtime();
+#endif
+            if (tid < 64) pt_reduced<T>(C.Sd, C.Sx, C.sp, shl, C.vb, C.sbv, true);
+            __syncthreads();
+#ifdef CMPC_STAMPS
+            if (tid == 0) { fst[12] += tc1 - tc0; fst[13] += tc2 - tc1; fst[14] += __builtin_amdgcn_s_memtime() - tc2; }
+            if (tid == 64) fst[15] += tc1 - tc0;   // an interior chain
+#endif
+        } else {
+            if (NTT >= 128) {   // one end per wave (waves 0 and 1)
+                if (tid < 128) tw_factor_ends<T, 64>(C.Sd, C.So, NB, NBm, shl, C.vb, fst);
+            } else {            // one end per half of wave 0
+                tw_factor_ends<T, 32>(C.Sd, C.So, NB, NBm, shl, C.vb, fst);
+            }
+            __syncthreads();
+            if (tid < 64) tw_factor_meet<T>(C.Sd, C.So, NBm, shl, C.vb);
+            __syncthreads();
         }
-        __syncthreads();
-        if (tid < 64) tw_factor_meet<T>(C.Sd, C.So, NBm, shl, C.vb);
-        __syncthreads();
         STAMP(3);
         // ---- predictor (affine) and corrector
         T sigma_mu = T(0);
@@ -2133,15 +2204,9 @@ __global__ void __launch_bounds__(NTT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int o
                 }
                 STAMP(4);
                 STAMP(5);   // (the right-hand side is formed inside phase_w)
-                if (tid < 64) tw_solve_elim<T>(C.So, NB, NBm, C.vb, ring);
-                __syncthreads();
-                if (tid < 64) tw_solve_meet<T>(C.Sd, C.So, NB, NBm, C.vb, shl);
-                __syncthreads();
+                schur_forward<T, NTT>(C, NB, NBm, ring, shl);
             }
-            tw_solve_local<T, NTT>(C.Sd, NB, NBm, C.vb);
-            __syncthreads();
-            if (tid < 64) tw_solve_back<T>(C.So, NB, NBm, C.vb, ring);
-            __syncthreads();
+            schur_backward<T, NTT>(C, NB, NBm, ring);
             STAMP(6);
             T am[1] = {T(1)}, mus[3] = {T(0), T(0), T(0)};
             for (int k = tid; k < K1; k += NTT) am[0] = fmin(am[0], phase_dz<T, ROBOT>(C, k, corr, init, mus));
@@ -2227,7 +2292,8 @@ __global__ void __launch_bounds__(NTT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int o
 
 #define INST(T, R)                                                                       \
     template __global__ void k_qp_ipm<T, R, 64>(DevBuf<T>, int, int, T, T, T, T, T);     \
-    template __global__ void k_qp_ipm<T, R, 128>(DevBuf<T>, int, int, T, T, T, T, T);
+    template __global__ void k_qp_ipm<T, R, 128>(DevBuf<T>, int, int, T, T, T, T, T);    \
+    template __global__ void k_qp_ipm<T, R, 256>(DevBuf<T>, int, int, T, T, T, T, T);
 INST(double, 0)
 INST(double, 1)
 INST(float, 0)
@@ -2236,8 +2302,10 @@ INST(float, 1)
 
 size_t ipm_lds_bytes(int N, int prec_bytes, int nt) {
     const size_t vec = (((size_t)(N + 2) * 9 + 7) & ~size_t(7));
-    // + the w_x side array; at least one covariance scan's buffers (the scan jobs after the QP)
-    return std::max<size_t>(vec + (size_t)2 * SWEEP_LDS + (nt > 64 ? vec : 0), SCAN_LDS) * prec_bytes;
+    // vb, the sweep rings (two; one per wave with four waves), the w_x side array, the fill
+    // products of the four-wave solves; at least one covariance scan's buffers (the scan jobs)
+    const size_t nring = nt >= 256 ? 4 : 2;
+    return std::max<size_t>(vec + nring * SWEEP_LDS + (nt > 64 ? vec : 0) + (nt >= 256 ? vec : 0), SCAN_LDS) * prec_bytes;
 }
 
 size_t ipm_workspace_elems(int N, int robot) {

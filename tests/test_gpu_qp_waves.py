@@ -53,13 +53,47 @@ def test_two_wave_workgroup_matches_one_wave(cfg, N, B):
         assert err.max() <= (1e-5 if talos else 1e-9), err.max()
 
 
+@pytest.mark.parametrize('cfg,N,B', [('trot', 40, 8), ('trot', 100, 64), ('trot', 255, 4), ('bound', 100, 8),
+                                     ('talos', 200, 16), ('pace', 150, 8)])
+def test_four_wave_partitioned_recurrence(cfg, N, B):
+    """Four-wave workgroups factor the Schur system as four chains around three separators
+    (schur_pt.hpp), a different elimination order from the two-ended recurrence, so results agree
+    to rounding: every QP solved, Newton counts within one (TALOS two), SCP decisions equal,
+    solutions within 1e-7 (TALOS 1e-5) of the one-wave kernel's, and the first and last problems
+    within 1e-5 of the oracle's sparse IPM on the exported QP."""
+    from oracle.sparse_ipm import solve_qp as sparse_ipm_qp
+    pb = make_batch(cfg, N, B, seed_offset=41)
+    one, four = _run(pb, 1), _run(pb, 4)
+    talos = cfg == 'talos'
+    for (z1, s1, i1, d1), (z4, s4, i4, d4) in zip(one, four):
+        assert np.all(s1 == 1) and np.all(s4 == 1), (s1, s4)
+        assert np.abs(i1 - i4).max() <= (2 if talos else 1), (i1, i4)
+        np.testing.assert_array_equal(d1, d4)
+        err = np.abs(z1 - z4).max(axis=1) / np.abs(z1).max(axis=1)
+        assert err.max() <= (1e-5 if talos else 1e-7), err.max()
+    s = Solver(pb.robot, N, B, 'fp64')
+    s.set_qp_settings(waves_per_problem=4)
+    s.upload(pb)
+    s.scp_iterate(fixed_iters=True)
+    z, _, st, _ = s.qp_solution(with_y=False)
+    nx = 9 * (N + 1)
+    for b in (0, B - 1):
+        P, q, A, l, u = s.export_qp(b)
+        ref = sparse_ipm_qp(P, q, A, l, u)
+        assert np.abs(z[b][:nx] - ref.x[:nx]).max() / np.abs(ref.x[:nx]).max() <= 1e-5
+    s.close()
+
+
 def test_waves_setting_is_validated():
-    """waves_per_problem: 0 (auto, the default), 1 or 2; anything else is refused."""
+    """waves_per_problem: 0 (auto, the default), 1, 2 or 4; anything else is refused."""
     pb = make_batch('trot', 20, 2)
     s = Solver(pb.robot, 20, 2, 'fp64')
     s.set_qp_settings(waves_per_problem=0)
+    s.set_qp_settings(waves_per_problem=4)
     with pytest.raises(Exception):
         s.set_qp_settings(waves_per_problem=3)
+    with pytest.raises(Exception):
+        s.set_qp_settings(waves_per_problem=8)
     s.close()
 
 
