@@ -45,3 +45,33 @@ def test_overlapped_scan_matches_in_order(cfg, N, B, stochastic):
         np.testing.assert_array_equal(fused[k], plain[k], err_msg=k)
     np.testing.assert_array_equal(lin_f['Sigma'], lin_p['Sigma'])
     assert np.abs(lin_f['Sigma'][:, -1]).max() > 0   # the scan ran to the last knot
+
+
+@pytest.mark.parametrize('N,B', [(100, 1024), (100, 256)])
+def test_overlapped_scan_early_exit_path(N, B):
+    """The reference's early-exit loop (fixed_iters=False, only the active problems iterate): every
+    other problem gets a tiny trust-region radius and keeps rejecting, the rest accept at the first
+    iteration and leave the loop.  With problems inactive, the QP workgroups of inactive problems
+    return before the scan-job loop (1024: scans inside the QP kernel) and the side-stream scan
+    skips them (256); X, U, K, Sigma must equal the phase-by-phase order bit for bit."""
+    pb = make_batch('trot', N, B, seed_offset=23)
+    radius = np.where(np.arange(B) % 2 == 0, 1e-9, pb.params[0].scp_params['trust_region_radius0'])
+
+    def run(fused):
+        s = Solver(pb.robot, N, B, 'fp64')
+        s.upload(pb)
+        s.set_trust_region(radius=radius)
+        for _ in range(3):
+            if fused:
+                s.scp_iterate(fixed_iters=False)
+            else:
+                s.linearize(); s.assemble(); s.qp_solve(); s.accept(fixed_iters=False)
+        sol = s.solution()
+        s.close()
+        return sol
+
+    f, p = run(True), run(False)
+    assert np.all(f['n_accepted'][1::2] == 1) and np.all(f['n_accepted'][0::2] == 0)
+    assert np.all(f['iterations'][1::2] == 1) and np.all(f['iterations'][0::2] == 3)
+    for k in ('X', 'U', 'K', 'Sigma', 'iterations', 'status', 'weight', 'radius'):
+        np.testing.assert_array_equal(f[k], p[k], err_msg=k)
