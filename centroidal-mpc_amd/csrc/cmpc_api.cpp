@@ -22,6 +22,10 @@ template <typename T, int R> __global__ void k_lin_knots(DevBuf<T>, int, int);
 template <typename T, int R> __global__ void k_cov_scan(DevBuf<T>, int);
 template <typename T, int R, bool FULL> __global__ void k_assemble(DevBuf<T>, int);
 template <typename T, int R, int NTT> __global__ void k_qp_ipm(DevBuf<T>, int, int, T, T, T, T, T);
+template <typename T, int R> __global__ void k_qp_pair(DevBuf<T>, const int *, int, int, int, T, T, T, T, T);
+template <typename T> __global__ void k_qp_order(DevBuf<T>, int, int *);
+size_t ipm_pair_lds_bytes(int N, int prec_bytes);
+int ipm_pair_max_batch();
 template <typename T> __global__ void k_interpolate(DevBuf<T>, int, int, T *, T *);
 template <typename T, int R> __global__ void k_contact_plan(DevBuf<T>, const cmpc_gait *, const T *, uint8_t *, T *, T *);
 template <typename T, int R> __global__ void k_default_controls(DevBuf<T>, T *);
@@ -102,9 +106,33 @@ template <typename T> DevParams<T> conv_params(const cmpc_params &p, int nw) {
 // Four waves (schur_pt.hpp: the Schur recurrence as four chains) when every problem still gets a
 // CU of its own and the horizon gives each chain a few blocks.
 int qp_waves(cmpc_handle h) {
+    if (const char *e = std::getenv("CMPC_QP_WAVES")) {   // diagnostic override (timing experiments)
+        const int w = std::atoi(e);
+        if (w == 1 || w == 2 || w == 4) return w;
+    }
     if (h->qs.waves_per_problem > 0) return h->qs.waves_per_problem == 4 && h->N < 16 ? 2 : h->qs.waves_per_problem;
     if (h->N >= 40 && (long)h->B <= (long)h->n_cu) return 4;
     return (h->N + 1 > 64 && 2L * h->B <= 4L * h->n_cu) ? 2 : 1;
+}
+
+// Paired QP workgroups (k_qp_pair: two problems per two-wave workgroup, both waves on whichever
+// problem is still running once the other has finished) in place of one wave per problem, for fp64
+// batches, when two such workgroups fit a CU's LDS and the batch fits k_qp_order.  Same-box A/B
+// (profiles/r03c_pair_ab.log): metric config QP 2.93 -> 2.75 ms (327k -> 348k SCP it/s); BASELINE
+// C3 (fp32, two Newton steps, no tail to balance) 0.744 -> 0.752 ms, so fp32 keeps one wave per
+// problem.  CMPC_QP_PAIR=0 turns them off (diagnostic A/B).
+bool qp_paired(cmpc_handle h) {
+    if (qp_waves(h) != 1 || h->B < 2 || h->B > ipm_pair_max_batch() || h->prec != CMPC_PREC_F64) return false;
+    if (const char *e = std::getenv("CMPC_QP_PAIR"))
+        if (e[0] == '0') return false;
+    return 2 * ipm_pair_lds_bytes(h->N, h->esz()) + 1024 <= 160 * 1024;
+}
+
+// CMPC_QP_PAIR=2: paired workgroups whose waves never share a problem (diagnostic: the cost of the
+// pairing itself)
+int qp_pair_share() {
+    const char *e = std::getenv("CMPC_QP_PAIR");
+    return e && e[0] == '2' ? 0 : 1;
 }
 
 // QP step fraction: the setting, or (0) the robot's. Same-box A/B, bench lines A B A B:
@@ -210,6 +238,25 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
         // (N+2) x 9 Schur vector and the sweep rings in LDS, the Schur blocks in the workspace
         const int nt = 64 * qp_waves(h);
         const T eta = T(qp_step_fraction(h));
+        if (qp_paired(h)) {
+            const size_t lds = ipm_pair_lds_bytes(h->N, (int)sizeof(T));
+            HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_qp_pair<T, R>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            if (h->scan_deferred) {   // the scans run in the QP's waves
+                HIPCHK(hipMemsetAsync(h->scan_ctr, 0, sizeof(unsigned), h->stream));
+                d.scan_ctr = (unsigned *)h->scan_ctr;
+                h->scan_deferred = false;
+            }
+            hipLaunchKernelGGL((k_qp_order<T>), dim3(1), dim3(1024), 0, h->stream, d, only_active, (int *)h->qp_order);
+            hipLaunchKernelGGL((k_qp_pair<T, R>), dim3((unsigned)((B + 1) / 2)), dim3(128), lds, h->stream, d,
+                               (const int *)h->qp_order, only_active, qp_pair_share(), h->qs.max_iter, T(h->qs.eps_abs),
+                               T(h->qs.eps_rel), eta, T(h->qs.init_floor_s), T(h->qs.init_floor_l));
+            if (h->scan_pending) {
+                HIPCHK(hipStreamWaitEvent(h->stream, h->ev_scan, 0));
+                h->scan_pending = false;
+            }
+            break;
+        }
         const size_t lds = ipm_lds_bytes(h->N, (int)sizeof(T), nt);
         const void *fn = nt == 256   ? reinterpret_cast<const void *>(&k_qp_ipm<T, R, 256>)
                          : nt == 128 ? reinterpret_cast<const void *>(&k_qp_ipm<T, R, 128>)
@@ -567,6 +614,7 @@ int cmpc_create(cmpc_handle *out, int device, int robot, int N, int max_batch, i
         HIPCHK(hipEventCreateWithFlags(&h->ev_pfK, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&h->ev_pfS, hipEventDisableTiming));
         h->scan_ctr = h->dalloc(16);
+        h->qp_order = h->dalloc(((size_t)max_batch + 1) * 4);
         HIPCHK(hipDeviceGetAttribute(&h->n_cu, hipDeviceAttributeMultiprocessorCount, device));
         for (auto &e : h->ev) HIPCHK(hipEventCreate(&e));
         const size_t Bm = max_batch, K1 = N + 1, NB = N + 2, e = h->esz(), NC = h->NC;

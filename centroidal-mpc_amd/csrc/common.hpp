@@ -144,18 +144,35 @@ template <typename T> __device__ __forceinline__ T wave_sum(T v) {
     return v;
 }
 
-// Block-wide reductions for blockDim.x == NT (multiple of 64).  `red` is LDS scratch of
-// at least NT/64 * NV elements.  All threads receive the result.
-template <typename T, int NT, int NV, int OP>   // OP: 0 sum, 1 max, 2 min
+// Barrier of a thread group of G threads inside a workgroup of WG threads (G, WG multiples of 64,
+// G | WG, groups aligned to G): the workgroup barrier when the group is the workgroup; a wave-level
+// barrier with workgroup-scope fences (the same waits on LDS and global memory as __syncthreads,
+// without the s_barrier the other waves of the workgroup are not part of) when it is one wave of
+// a larger workgroup (k_qp_pair: one problem per wave until one of them has finished).
+template <int G, int WG> __device__ __forceinline__ void gsync() {
+    static_assert(G == WG || G == 64, "a group is the workgroup or one of its waves");
+    if constexpr (G == WG) {
+        __syncthreads();
+    } else {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+}
+
+// Reductions over a group of NT threads (multiple of 64; the workgroup, or one wave of a larger one,
+// see gsync).  `red` is LDS scratch of at least NT/64 * NV elements, private to the group.  All
+// threads of the group receive the result.
+template <typename T, int NT, int NV, int OP, int WG = NT>   // OP: 0 sum, 1 max, 2 min
 __device__ __forceinline__ void block_reduce(T (&v)[NV], T *red) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wid = (threadIdx.x & (NT - 1)) >> 6;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
         T a = v[i];
         a = OP == 0 ? wave_sum(a) : OP == 1 ? wave_max(a) : wave_min(a);
         if (lane == 0) red[wid * NV + i] = a;
     }
-    __syncthreads();
+    gsync<NT, WG>();
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
         T a = red[i];
@@ -166,7 +183,7 @@ __device__ __forceinline__ void block_reduce(T (&v)[NV], T *red) {
         }
         v[i] = a;
     }
-    __syncthreads();
+    gsync<NT, WG>();
 }
 
 // skew(v) * x  == v cross x

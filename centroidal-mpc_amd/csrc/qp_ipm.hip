@@ -34,6 +34,12 @@
 #ifndef QP_MIN_WAVES
 #define QP_MIN_WAVES 1   // __launch_bounds__ waves per SIMD (2: 256 registers, four workgroups per CU)
 #endif
+#ifndef QP_MIN_WAVES_2W
+#define QP_MIN_WAVES_2W QP_MIN_WAVES   // the same for the two-wave kernel
+#endif
+#ifndef QP_KE
+#define QP_KE 8
+#endif
 
 namespace cmpc {
 
@@ -1282,7 +1288,7 @@ template <typename T, int K, bool PK = false> struct ChunkStream {   // PK: pack
         return buf + ((i / K) & 1) * K * RSLOT + (i % K) * RSLOT;
     }
 };
-constexpr int KE = 8;   // blocks per chunk of the sweep streams
+constexpr int KE = QP_KE;   // blocks per chunk of the sweep streams
 constexpr int SWEEP_LDS = 2 * KE * RSLOT;   // per half-wave: 2 x 8 slots = 2 x (2 x 4) slots
 
 // (5c) two-ended block sweeps with the twisted factors (one end per half-wave): rhs -> dnu in
@@ -1352,7 +1358,7 @@ __device__ void tw_solve_meet(const T *Ii, const T *Xs, int NB, int m, LdsT<T> *
 // parallel (thread per block, in place in vb) once the elimination and the meeting block are
 // done: the sequential step is then a single 9-term product.
 template <typename T, int NTT> __device__ void tw_solve_local(const T *Ii, int NB, int m, LdsT<T> *vb) {
-    for (int j = threadIdx.x; j < NB; j += NTT) {
+    for (int j = threadIdx.x & (NTT - 1); j < NB; j += NTT) {
         if (j == m) continue;
         const GlbT<T> *I = (const GlbT<T> *)Ii + (size_t)j * 81;   // packed
         T iv[45], y[9];
@@ -1541,7 +1547,7 @@ __device__ __forceinline__ void phase_w_core(const Ctx<T, ROBOT> &C, int k, int 
 }
 // the deferred last term of the fused right-hand side (multi-wave workgroups): block k += w_x,k
 template <typename T, int NTT> __device__ __forceinline__ void add_wx(LdsT<T> *vb, const LdsT<T> *wxs, int N) {
-    for (int e = 9 + (int)threadIdx.x; e < (N + 1) * 9; e += NTT) vb[e] += wxs[e];
+    for (int e = 9 + (int)(threadIdx.x & (NTT - 1)); e < (N + 1) * 9; e += NTT) vb[e] += wxs[e];
 }
 template <typename T, int ROBOT> __device__ __forceinline__ void phase_w(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu) {
     using S = Stage<ROBOT>;
@@ -1948,81 +1954,102 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_init_shift(con
 // Forward elimination + separator / meeting-block solve of the right-hand side in vb, and the back
 // substitution, with the factors of this Newton step: the two-ended recurrence (one or two waves)
 // or the four chains of schur_pt.hpp (four waves).  Barriers included.
-template <typename T, int NTT, typename CT>
+template <typename T, int NTT, int WG, typename CT>
 __device__ __forceinline__ void schur_forward(const CT &C, int NB, int NBm, LdsT<T> *ring, LdsT<T> *shl) {
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x & (NTT - 1);
     if constexpr (NTT >= 256) {
         pt_solve_elim<T>(C.So, NB, C.sp, C.vb, ring, C.sbv);
-        __syncthreads();
+        gsync<NTT, WG>();
         pt_fill_rhs<T, NTT>(C.Sh, C.sp, C.vb, C.hy);
-        __syncthreads();
+        gsync<NTT, WG>();
         if (tid < 64) {
             pt_fill_sum<T>(C.sp, C.hy, C.sbv);
             pt_reduced<T>(C.Sd, C.Sx, C.sp, shl, C.vb, C.sbv, false);
         }
-        __syncthreads();
+        gsync<NTT, WG>();
     } else {
         if (tid < 64) tw_solve_elim<T>(C.So, NB, NBm, C.vb, ring);
-        __syncthreads();
+        gsync<NTT, WG>();
         if (tid < 64) tw_solve_meet<T>(C.Sd, C.So, NB, NBm, C.vb, shl);
-        __syncthreads();
+        gsync<NTT, WG>();
     }
 }
-template <typename T, int NTT, typename CT>
+template <typename T, int NTT, int WG, typename CT>
 __device__ __forceinline__ void schur_backward(const CT &C, int NB, int NBm, LdsT<T> *ring) {
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x & (NTT - 1);
     if constexpr (NTT >= 256) {
         pt_solve_local<T, NTT>(C.Sd, C.Sh, NB, C.sp, C.vb);
-        __syncthreads();
+        gsync<NTT, WG>();
         pt_solve_back<T>(C.So, NB, C.sp, C.vb, ring);
-        __syncthreads();
+        gsync<NTT, WG>();
     } else {
         tw_solve_local<T, NTT>(C.Sd, NB, NBm, C.vb);
-        __syncthreads();
+        gsync<NTT, WG>();
         if (tid < 64) tw_solve_back<T>(C.So, NB, NBm, C.vb, ring);
-        __syncthreads();
+        gsync<NTT, WG>();
     }
 }
 
 // One step of iterative refinement of the corrector direction; returns the new step bound.
 // (Inlined: as an outlined call, the registers live across it were reloaded from scratch all over
 // the Newton step.)
-template <typename T, int ROBOT, int NTT>
+template <typename T, int ROBOT, int NTT, int WG>
 __device__ __forceinline__ T refine_direction(const Ctx<T, ROBOT> &C, T sigma_mu, LdsT<T> *ring, LdsT<T> *shl,
                                                         T *red) {
-    const int tid = threadIdx.x, K1 = C.N + 1, NB = C.N + 2, NBm = NB / 2;
+    const int tid = threadIdx.x & (NTT - 1), K1 = C.N + 1, NB = C.N + 2, NBm = NB / 2;
     for (int k = tid; k < K1; k += NTT) phase_lres<T, ROBOT>(C, k, sigma_mu);
-    __syncthreads();
+    gsync<NTT, WG>();
     for (int k = tid; k < K1; k += NTT) phase_w<T, ROBOT>(C, k, 2, T(0));
-    __syncthreads();
+    gsync<NTT, WG>();
     if (NTT > 64) {
         add_wx<T, NTT>(C.vb, C.wxs, C.N);
-        __syncthreads();
+        gsync<NTT, WG>();
     }
-    schur_forward<T, NTT>(C, NB, NBm, ring, shl);
-    schur_backward<T, NTT>(C, NB, NBm, ring);
+    schur_forward<T, NTT, WG>(C, NB, NBm, ring, shl);
+    schur_backward<T, NTT, WG>(C, NB, NBm, ring);
     T ar[1] = {T(1)};
     for (int k = tid; k < K1; k += NTT) ar[0] = fmin(ar[0], phase_dz_refine<T, ROBOT>(C, k));
-    block_reduce<T, NTT, 1, 2>(ar, red);   // (its barriers order the dnu reads before the sum)
+    block_reduce<T, NTT, 1, 2, WG>(ar, red);   // (its barriers order the dnu reads before the sum)
     for (int e = tid; e < NB * 9; e += NTT) C.vb[e] += C.ws[(WF(dn0) + e % 9) * KPC + e / 9];
-    __syncthreads();
+    gsync<NTT, WG>();
     return ar[0];
 }
 
-// ------------------------------------------------------------------ kernel
-template <typename T, int ROBOT, int NTT>
-__global__ void __launch_bounds__(NTT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int only_active, int max_iter, T eps_abs, T eps_rel,
-                                               T eta, T floor_s, T floor_l) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char dsmem[];
-    constexpr int NI = Rows<ROBOT>::NI;
-    const int b = blockIdx.x;
-    if (b >= d.B) return;
-    if (only_active && !d.scp[b].active) return;
-    __shared__ T red[8 * (NTT / 64)];
-    __shared__ T sh[NTT >= 256 ? 4 * PT_SCRATCH : 2 * TW_SCRATCH];
-    __shared__ T sbv_s[NTT >= 256 ? 6 * 9 : 1];
-    const int tid = threadIdx.x, N = d.N, K1 = N + 1, NB = N + 2, NBm = NB / 2;
-    Ctx<T, ROBOT> C{N, nullptr, nullptr, nullptr, nullptr, T(0), T(0), nullptr, nullptr, nullptr, nullptr, T(0), T(0), T(0), nullptr};
+// ------------------------------------------------------------------ kernels
+// Newton-loop state of one problem's solve (carried across k_qp_pair's change of mode)
+template <typename T> struct IpmState {
+    int status, it, stall, n_refine, yielded;
+    T mu_prev, merit, prim_prev;
+#ifdef CMPC_STAMPS
+    unsigned long long t_acc[12];
+#endif
+};
+template <typename T> __device__ __forceinline__ IpmState<T> ipm_state0() {
+    IpmState<T> S;
+    S.status = CMPC_QP_MAX_ITER;
+    S.it = S.stall = S.n_refine = S.yielded = 0;
+    S.mu_prev = T(-1);
+    S.merit = S.prim_prev = T(0);
+#ifdef CMPC_STAMPS
+    for (int i = 0; i < 12; ++i) S.t_acc[i] = 0;
+#endif
+    return S;
+}
+
+// LDS of one solve besides what Ctx points to: this thread's sweep ring, the recurrence scratch
+// of the two ends, the reduction scratch (private to the group)
+template <typename T> struct IpmLds {
+    LdsT<T> *ring, *shl;
+    T *red;
+};
+
+// Problem b's context; its cost weights and contact masks copied by the group's G threads into
+// the given LDS slots (the caller syncs the group before they are read)
+template <typename T, int ROBOT, int G>
+__device__ __forceinline__ void ctx_setup(const DevBuf<T> &d, int b, Ctx<T, ROBOT> &C, LdsT<T> *wts, LdsT<uint8_t> *cms,
+                                          T floor_s, T floor_l) {
+    const int tid = threadIdx.x & (G - 1), N = d.N, K1 = N + 1;
+    C.N = N;
     C.prm = d.params + d.class_id[b];
     C.stage = d.stage + (size_t)b * Stage<ROBOT>::SIZE * KPC;
     C.logic = d.logic + (size_t)b * N * Robot<ROBOT>::NC;
@@ -2037,46 +2064,24 @@ __global__ void __launch_bounds__(NTT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int o
         C.dcap = T(1e12) * wmax;
     }
     C.ws = d.ws + (size_t)b * d.ws_stride;
-    __shared__ T wts[18 + 2 * NU];
     if (tid < 9) { wts[tid] = C.prm->Wx[tid]; wts[9 + tid] = T(1) / C.prm->Wx[tid]; }
     if (tid < NU) { wts[18 + tid] = C.prm->Wu[tid]; wts[18 + NU + tid] = T(1) / C.prm->Wu[tid]; }
-    C.wt = (const LdsT<T> *)wts;
+    C.wt = wts;
     // contact masks of every knot, once per solve (each phase read them from global memory
     // first thing, and everything after waited on that load)
-    __shared__ uint8_t cms[KPC];
-    for (int k = tid; k < K1; k += NTT) cms[k] = (uint8_t)C.cmask_mem(k);
-    C.cm = (const LdsT<uint8_t> *)cms;
-    __syncthreads();
-    // dynamic LDS: the (N+2) x 9 Schur vector, then two block rings per wave for the sweeps
-    LdsT<T> *shl = (LdsT<T> *)sh;
-    C.vb = (LdsT<T> *)reinterpret_cast<T *>(dsmem);
-    // rings: one per half-wave of wave 0 (two-ended sweeps), one per wave (four-wave chains)
-    constexpr int NRING = NTT >= 256 ? 4 : 2;
-    const int vec = (NB * 9 + 7) & ~7;
-    LdsT<T> *ring = C.vb + vec + (NTT >= 256 ? (tid >> 6) : ((tid & 63) >> 5)) * SWEEP_LDS;
-    if (NTT > 64) C.wxs = C.vb + vec + NRING * SWEEP_LDS;
+    C.cm = nullptr;
+    for (int k = tid; k < K1; k += G) cms[k] = (uint8_t)C.cmask_mem(k);
+    C.cm = cms;
     C.Sd = C.ws + Ws<ROBOT>::Sd;
     C.So = C.ws + Ws<ROBOT>::So;
-    if (NTT >= 256) {
-        C.Sh = C.ws + Ws<ROBOT>::Sh;
-        C.Sx = C.ws + Ws<ROBOT>::Sx;
-        pt_seps<T>(NB, C.sp);
-        C.sbv = (LdsT<T> *)sbv_s;
-        C.hy = C.wxs + vec;
-    }
-#ifdef CMPC_STAMPS
-    unsigned long long t_prev = __builtin_amdgcn_s_memtime(), t_acc[12] = {};
-#define STAMP(i)                                                               \
-    do {                                                                       \
-        const unsigned long long t_now = __builtin_amdgcn_s_memtime();         \
-        t_acc[i] += t_now - t_prev;                                            \
-        t_prev = t_now;                                                        \
-    } while (0)
-#else
-#define STAMP(i) do { } while (0)
-#endif
-    // ---- starting point of the initialization step: z = (xlin, ulin, 0), nu = 0, s = lambda = 1
-    for (int k = tid; k < K1; k += NTT) {
+}
+
+// Starting point of the initialization step: z = (xlin, ulin, 0), nu = 0, s = lambda = 1
+template <typename T, int ROBOT, int G, int WG>
+__device__ __forceinline__ void ipm_start(const DevBuf<T> &d, const Ctx<T, ROBOT> &C, int b) {
+    constexpr int NI = Rows<ROBOT>::NI;
+    const int tid = threadIdx.x & (G - 1), N = C.N, K1 = N + 1, NB = N + 2;
+    for (int k = tid; k < K1; k += G) {
         const SV<T> x = C.var_x(k);
         const T *xl = d.Xlin + ((size_t)b * K1 + k) * 9;   // start at the linearization point
         const T *ubar = d.Ulin + ((size_t)b * N + (k < N ? k : 0)) * NU;
@@ -2095,24 +2100,48 @@ __global__ void __launch_bounds__(NTT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int o
             dla[r] = T(0);
         }
     }
-    for (int j = tid; j < NB; j += NTT) {
+    for (int j = tid; j < NB; j += G) {
         const SV<T> nu = C.bv(WF(nu), j);
         for (int i = 0; i < 9; ++i) nu[i] = T(0);
     }
-    __syncthreads();
-    int status = CMPC_QP_MAX_ITER, it = 0, stall = 0, n_refine = 0;
-    T mu_prev = T(-1), merit = T(0), prim_prev = T(0);
+    gsync<G, WG>();
+}
+
+// Newton iterations of problem b on a group of G threads (the workgroup, or one wave of a WG-thread
+// workgroup), from S.it until the stopping test, a failure exit or the cap; with `yield` set, the
+// loop also leaves (S.yielded) at the top of an iteration once *yield is nonzero.
+template <typename T, int ROBOT, int G, int WG>
+__device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT> &C, int b, IpmState<T> &S,
+                                         const IpmLds<T> &L, int max_iter, T eps_abs, T eps_rel, T eta,
+                                         const volatile LdsT<int> *yield) {
+    const int tid = threadIdx.x & (G - 1), N = C.N, K1 = N + 1, NB = N + 2, NBm = NB / 2;
+    (void)b;
+#ifdef CMPC_STAMPS
+    unsigned long long t_prev = __builtin_amdgcn_s_memtime();
+#define STAMP(i)                                                               \
+    do {                                                                       \
+        const unsigned long long t_now = __builtin_amdgcn_s_memtime();         \
+        S.t_acc[i] += t_now - t_prev;                                          \
+        t_prev = t_now;                                                        \
+    } while (0)
+#else
+#define STAMP(i) do { } while (0)
+#endif
+    int status = S.status, it = S.it, stall = S.stall, n_refine = S.n_refine;
+    T mu_prev = S.mu_prev, merit = S.merit, prim_prev = S.prim_prev;
     // it == 0 is the initialization step: one full Newton step from s = lambda = 1 gives an
     // equality-feasible least-squares start; s and lambda are then floored row by row (Solo12)
     // or shifted by 1 + the largest violation (TALOS), see init_s_knot.
-    for (it = 0; it <= max_iter; ++it) {
+    for (it = S.it; it <= max_iter; ++it) {
+        // k_qp_pair: the partner wave has finished, so this problem continues on both waves
+        if (yield && __builtin_amdgcn_readfirstlane(*yield)) { S.yielded = 1; break; }
         const bool init = (it == 0);
         Norms<T, ROBOT> nm{0, 0, 0, 0, 0, 0, 0, 0};
-        for (int k = tid; k < K1; k += NTT) phase_residual<T, ROBOT>(C, k, nm);
+        for (int k = tid; k < K1; k += G) phase_residual<T, ROBOT>(C, k, nm);
         T mx[6] = {nm.prim, nm.dual, nm.comp, nm.sp, nm.sd, nm.lmax};
-        block_reduce<T, NTT, 6, 1>(mx, red);
+        block_reduce<T, G, 6, 1, WG>(mx, L.red);
         T sm2[2] = {nm.mu, nm.cnt};
-        block_reduce<T, NTT, 2, 0>(sm2, red);
+        block_reduce<T, G, 2, 0, WG>(sm2, L.red);
         STAMP(0);
         const T prim = mx[0], dual = mx[1], comp = mx[2], sp = mx[3], sdd = mx[4];
         const T mu = sm2[0] / fmax(sm2[1], T(1));
@@ -2126,9 +2155,9 @@ __global__ void __launch_bounds__(NTT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int o
             // |E'nu + G'lambda| <= eps |(nu, lambda)| and b'nu + h'lambda <= -eps |(nu, lambda)|
             if (it >= 3 && prim > T(0.9) * prim_prev && merit > T(1e3)) {
                 T cm[2] = {T(0), mx[5]}, cs[1] = {T(0)};
-                for (int k = tid; k < K1; k += NTT) phase_cert<T, ROBOT>(C, k, cm, cs[0]);
-                block_reduce<T, NTT, 2, 1>(cm, red);
-                block_reduce<T, NTT, 1, 0>(cs, red);
+                for (int k = tid; k < K1; k += G) phase_cert<T, ROBOT>(C, k, cm, cs[0]);
+                block_reduce<T, G, 2, 1, WG>(cm, L.red);
+                block_reduce<T, G, 1, 0, WG>(cs, L.red);
                 if (cm[0] <= T(QP_EPS_PINF) * cm[1] && cs[0] <= -T(QP_EPS_PINF) * cm[1]) {
                     status = CMPC_QP_PRIMAL_INFEASIBLE;
                     break;
@@ -2144,17 +2173,17 @@ __global__ void __launch_bounds__(NTT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int o
         if (it == max_iter) break;
         // ---- Phi factors and the predictor's particular solution (knot-local), then the S blocks
         // and the predictor's Schur right-hand side
-        for (int k = tid; k < K1; k += NTT) {
+        for (int k = tid; k < K1; k += G) {
             KnotSL<T, ROBOT> kl;
             load_knot_sl(C, k, kl);
             phase_factor<T, ROBOT>(C, k, kl);
             phase_w_pred<T, ROBOT>(C, k, kl);
         }
-        __syncthreads();
+        gsync<G, WG>();
         STAMP(1);
-        if (NTT > 64) add_wx<T, NTT>(C.vb, C.wxs, N);
-        for (int k = tid; k < K1; k += NTT) phase_sblock<T, ROBOT>(C, k);
-        __syncthreads();
+        if (G > 64) add_wx<T, G>(C.vb, C.wxs, N);
+        for (int k = tid; k < K1; k += G) phase_sblock<T, ROBOT>(C, k);
+        gsync<G, WG>();
         STAMP(2);
         // ---- factorization of S with the predictor's forward elimination fused in
 #ifdef CMPC_STAMPS
@@ -2162,33 +2191,33 @@ __global__ void __launch_bounds__(NTT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int o
 #else
         unsigned long long *fst = nullptr;
 #endif
-        if (NTT >= 256) {   // four chains and the separator system (schur_pt.hpp)
+        if (G >= 256) {   // four chains and the separator system (schur_pt.hpp)
 #ifdef CMPC_STAMPS
             const unsigned long long tc0 = __builtin_amdgcn_s_memtime();
 #endif
-            pt_factor_chains<T>(C.Sd, C.So, C.Sh, C.Sx, NB, C.sp, shl + (tid >> 6) * PT_SCRATCH, C.vb, C.sbv);
+            pt_factor_chains<T>(C.Sd, C.So, C.Sh, C.Sx, NB, C.sp, L.shl + (tid >> 6) * PT_SCRATCH, C.vb, C.sbv);
 #ifdef CMPC_STAMPS
             const unsigned long long tc1 = __builtin_amdgcn_s_memtime();
 #endif
-            __syncthreads();
+            gsync<G, WG>();
 #ifdef CMPC_STAMPS
             const unsigned long long tc2 = __builtin_amdgcn_s_memtime();
 #endif
-            if (tid < 64) pt_reduced<T>(C.Sd, C.Sx, C.sp, shl, C.vb, C.sbv, true);
-            __syncthreads();
+            if (tid < 64) pt_reduced<T>(C.Sd, C.Sx, C.sp, L.shl, C.vb, C.sbv, true);
+            gsync<G, WG>();
 #ifdef CMPC_STAMPS
             if (tid == 0) { fst[12] += tc1 - tc0; fst[13] += tc2 - tc1; fst[14] += __builtin_amdgcn_s_memtime() - tc2; }
             if (tid == 64) fst[15] += tc1 - tc0;   // an interior chain
 #endif
         } else {
-            if (NTT >= 128) {   // one end per wave (waves 0 and 1)
-                if (tid < 128) tw_factor_ends<T, 64>(C.Sd, C.So, NB, NBm, shl, C.vb, fst);
+            if (G >= 128) {   // one end per wave (waves 0 and 1)
+                if (tid < 128) tw_factor_ends<T, 64>(C.Sd, C.So, NB, NBm, L.shl, C.vb, fst);
             } else {            // one end per half of wave 0
-                tw_factor_ends<T, 32>(C.Sd, C.So, NB, NBm, shl, C.vb, fst);
+                tw_factor_ends<T, 32>(C.Sd, C.So, NB, NBm, L.shl, C.vb, fst);
             }
-            __syncthreads();
-            if (tid < 64) tw_factor_meet<T>(C.Sd, C.So, NBm, shl, C.vb);
-            __syncthreads();
+            gsync<G, WG>();
+            if (tid < 64) tw_factor_meet<T>(C.Sd, C.So, NBm, L.shl, C.vb);
+            gsync<G, WG>();
         }
         STAMP(3);
         // ---- predictor (affine) and corrector
@@ -2196,26 +2225,26 @@ __global__ void __launch_bounds__(NTT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int o
         T alpha = T(1);
         for (int corr = 0; corr < 2; ++corr) {
             if (corr) {
-                for (int k = tid; k < K1; k += NTT) phase_w<T, ROBOT>(C, k, corr, sigma_mu);
-                __syncthreads();
-                if (NTT > 64) {
-                    add_wx<T, NTT>(C.vb, C.wxs, N);
-                    __syncthreads();
+                for (int k = tid; k < K1; k += G) phase_w<T, ROBOT>(C, k, corr, sigma_mu);
+                gsync<G, WG>();
+                if (G > 64) {
+                    add_wx<T, G>(C.vb, C.wxs, N);
+                    gsync<G, WG>();
                 }
                 STAMP(4);
                 STAMP(5);   // (the right-hand side is formed inside phase_w)
-                schur_forward<T, NTT>(C, NB, NBm, ring, shl);
+                schur_forward<T, G, WG>(C, NB, NBm, L.ring, L.shl);
             }
-            schur_backward<T, NTT>(C, NB, NBm, ring);
+            schur_backward<T, G, WG>(C, NB, NBm, L.ring);
             STAMP(6);
             T am[1] = {T(1)}, mus[3] = {T(0), T(0), T(0)};
-            for (int k = tid; k < K1; k += NTT) am[0] = fmin(am[0], phase_dz<T, ROBOT>(C, k, corr, init, mus));
-            block_reduce<T, NTT, 1, 2>(am, red);
+            for (int k = tid; k < K1; k += G) am[0] = fmin(am[0], phase_dz<T, ROBOT>(C, k, corr, init, mus));
+            block_reduce<T, G, 1, 2, WG>(am, L.red);
             STAMP(7);
             alpha = am[0];
             if (init) break;
             if (corr == 0) {   // Mehrotra centering from the affine step's complementarity
-                block_reduce<T, NTT, 3, 0>(mus, red);
+                block_reduce<T, G, 3, 0, WG>(mus, L.red);
                 const T mu_aff = (mus[0] + alpha * (mus[1] + alpha * mus[2])) / fmax(sm2[1], T(1));
                 const T sg = mu_aff / fmax(mu, std::numeric_limits<T>::min());
                 sigma_mu = sg * sg * sg * mu;
@@ -2224,29 +2253,43 @@ __global__ void __launch_bounds__(NTT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int o
                 // one step of iterative refinement of the corrector direction (residual of the
                 // Newton system with the exact operators, correction solved with the same
                 // factorization; see oracle/ipm_mirror.py)
-                alpha = refine_direction<T, ROBOT, NTT>(C, sigma_mu, ring, shl, red);
+                alpha = refine_direction<T, ROBOT, G, WG>(C, sigma_mu, L.ring, L.shl, L.red);
                 ++n_refine;
             }
         }
         if (init) {
             T vmax[2] = {T(-1e300), T(-1e300)};
-            for (int k = tid; k < K1; k += NTT) phase_init_step<T, ROBOT>(C, k, vmax);
+            for (int k = tid; k < K1; k += G) phase_init_step<T, ROBOT>(C, k, vmax);
             if (ROBOT == 1 || !(C.fls > T(0))) {   // CVXOPT shift (Solo12 floors inside init_s_knot)
-                block_reduce<T, NTT, 2, 1>(vmax, red);
+                block_reduce<T, G, 2, 1, WG>(vmax, L.red);
                 const T sh_s = vmax[0] >= T(0) ? T(1) + vmax[0] : T(0);
                 const T sh_l = vmax[1] >= T(0) ? T(1) + vmax[1] : T(0);
-                for (int k = tid; k < K1; k += NTT) phase_init_shift<T, ROBOT>(C, k, sh_s, sh_l);
+                for (int k = tid; k < K1; k += G) phase_init_shift<T, ROBOT>(C, k, sh_s, sh_l);
             }
-            __syncthreads();
+            gsync<G, WG>();
             continue;
         }
         alpha = fmin(T(1), eta * alpha);
-        for (int k = tid; k < K1; k += NTT) phase_update<T, ROBOT>(C, k, alpha);
-        __syncthreads();
+        for (int k = tid; k < K1; k += G) phase_update<T, ROBOT>(C, k, alpha);
+        gsync<G, WG>();
         STAMP(8);
     }
-    // ---- outputs: solution and multipliers
-    for (int k = tid; k < K1; k += NTT) {
+    S.status = status;
+    S.it = it;
+    S.stall = stall;
+    S.n_refine = n_refine;
+    S.mu_prev = mu_prev;
+    S.merit = merit;
+    S.prim_prev = prim_prev;
+#undef STAMP
+}
+
+// Solution, multipliers and exit record of problem b
+template <typename T, int ROBOT, int G>
+__device__ __forceinline__ void ipm_finish(const DevBuf<T> &d, const Ctx<T, ROBOT> &C, int b, const IpmState<T> &S) {
+    constexpr int NI = Rows<ROBOT>::NI;
+    const int tid = threadIdx.x & (G - 1), N = C.N, K1 = N + 1, NB = N + 2;
+    for (int k = tid; k < K1; k += G) {
         T x[9], u[NU], lm[NI];
         ldv(C.var_x(k), x);
         ldv(C.var_u(k), u);
@@ -2258,16 +2301,56 @@ __global__ void __launch_bounds__(NTT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int o
         for (int r = 0; r < NI; ++r)
             d.lams[((size_t)b * K1 + k) * NI + r] = Ctx<T, ROBOT>::present_m(msk, r) ? lm[r] : T(0);
     }
-    for (int e = tid; e < NB * 9; e += NTT) d.nus[(size_t)b * NB * 9 + e] = C.ws[(WF(nu) + e % 9) * KPC + e / 9];
+    for (int e = tid; e < NB * 9; e += G) d.nus[(size_t)b * NB * 9 + e] = C.ws[(WF(nu) + e % 9) * KPC + e / 9];
     if (tid == 0) {
-        d.qp_status[b] = status;
-        d.qp_iters[b] = it;
-        d.qp_merit[b] = merit;
-        d.qp_nref[b] = n_refine;
+        d.qp_status[b] = S.status;
+        d.qp_iters[b] = S.it;
+        d.qp_merit[b] = S.merit;
+        d.qp_nref[b] = S.n_refine;
 #ifdef CMPC_STAMPS
-        for (int i = 0; i < 9; ++i) d.stamps[(size_t)b * 16 + i] = t_acc[i];   // 9..11: k_linearize, 12..15: tw_factor_ends
+        for (int i = 0; i < 9; ++i) d.stamps[(size_t)b * 16 + i] = S.t_acc[i];   // 9..11: k_linearize, 12..15: tw_factor_ends
 #endif
     }
+}
+
+// One workgroup per problem: one, two or four waves (cmpc_api.cpp qp_waves).
+template <typename T, int ROBOT, int NTT>
+__global__ void __launch_bounds__(NTT, NTT == 128 ? QP_MIN_WAVES_2W : QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int only_active, int max_iter, T eps_abs, T eps_rel,
+                                               T eta, T floor_s, T floor_l) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char dsmem[];
+    const int b = blockIdx.x;
+    if (b >= d.B) return;
+    if (only_active && !d.scp[b].active) return;
+    __shared__ T red[8 * (NTT / 64)];
+    __shared__ T sh[NTT >= 256 ? 4 * PT_SCRATCH : 2 * TW_SCRATCH];
+    __shared__ T sbv_s[NTT >= 256 ? 6 * 9 : 1];
+    __shared__ T wts[18 + 2 * NU];
+    __shared__ uint8_t cms[KPC];
+    const int tid = threadIdx.x, N = d.N, NB = N + 2;
+    Ctx<T, ROBOT> C{};
+    ctx_setup<T, ROBOT, NTT>(d, b, C, (LdsT<T> *)wts, (LdsT<uint8_t> *)cms, floor_s, floor_l);
+    __syncthreads();
+    // dynamic LDS: the (N+2) x 9 Schur vector, then two block rings per wave for the sweeps
+    C.vb = (LdsT<T> *)reinterpret_cast<T *>(dsmem);
+    // rings: one per half-wave of wave 0 (two-ended sweeps), one per wave (four-wave chains)
+    constexpr int NRING = NTT >= 256 ? 4 : 2;
+    const int vec = (NB * 9 + 7) & ~7;
+    IpmLds<T> L;
+    L.ring = C.vb + vec + (NTT >= 256 ? (tid >> 6) : ((tid & 63) >> 5)) * SWEEP_LDS;
+    L.shl = (LdsT<T> *)sh;
+    L.red = red;
+    if (NTT > 64) C.wxs = C.vb + vec + NRING * SWEEP_LDS;
+    if (NTT >= 256) {
+        C.Sh = C.ws + Ws<ROBOT>::Sh;
+        C.Sx = C.ws + Ws<ROBOT>::Sx;
+        pt_seps<T>(NB, C.sp);
+        C.sbv = (LdsT<T> *)sbv_s;
+        C.hy = C.wxs + vec;
+    }
+    IpmState<T> S = ipm_state0<T>();
+    ipm_start<T, ROBOT, NTT, NTT>(d, C, b);
+    ipm_loop<T, ROBOT, NTT, NTT>(d, C, b, S, L, max_iter, eps_abs, eps_rel, eta, nullptr);
+    ipm_finish<T, ROBOT, NTT>(d, C, b, S);
     // Covariance scans of a deterministic batch (cmpc_api.cpp launch_phase): a workgroup whose QP
     // has finished takes scan jobs from the counter until none is left, so the scans fill the
     // SIMDs of problems that converged early.  Every workgroup leaves after one failed take.  Only
@@ -2287,18 +2370,189 @@ __global__ void __launch_bounds__(NTT, QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int o
             if (tid < 64) cov_scan_problem<T, ROBOT>(d, j, scan_lds);
         }
     }
-#undef STAMP
+}
+
+// ------------------------------------------------------------------ paired problems
+// Batches of one wave per problem (the metric config: 1024 problems, one per SIMD) last as long as
+// their slowest problem: trot N=100 x 1024 takes 4 to 7 Newton steps per problem, so the SIMD of a
+// 4-step problem idles for three steps.  k_qp_pair holds two problems per two-wave workgroup,
+// one per wave (the one-wave algorithm, ipm_loop<.., 64, 128>); once one of them has finished, the
+// other leaves its loop at the top of its next iteration and both waves finish it with the
+// two-wave algorithm (ipm_loop<.., 128, 128>: one knot per thread, one end of the Schur
+// recurrence per wave).  k_qp_order pairs the problems that took the most Newton steps in the
+// previous QP launch with those that took the fewest (inactive problems count zero).
+//
+// LDS of one wave's problem (elements of T): Schur vector | two sweep rings (the two halves of
+// the wave) | recurrence scratch of the two ends | reductions | cost weights | contact masks.  In
+// the two-wave mode the remaining problem keeps its region, and the other one's Schur-vector slot
+// holds the w_x side array (add_wx).
+template <typename T> struct PairLds {
+    static constexpr int RING = 2 * SWEEP_LDS, SH = 2 * TW_SCRATCH, RED = 16, WTS = 48;
+    static constexpr int CMS = (KPC + 8 * (int)sizeof(T) - 1) / (8 * (int)sizeof(T)) * 8;
+    __host__ __device__ static constexpr int vec(int N) { return ((N + 2) * 9 + 7) & ~7; }
+    __host__ __device__ static constexpr int region(int N) { return vec(N) + RING + SH + RED + WTS + CMS; }
+};
+
+template <typename T, int ROBOT>
+__global__ void __launch_bounds__(128, 1) k_qp_pair(DevBuf<T> d, const int *order, int only_active, int share,
+                                                    int max_iter, T eps_abs, T eps_rel, T eta, T floor_s, T floor_l) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char dsmem[];
+    using PL = PairLds<T>;
+    __shared__ int flag[2], rem;
+    __shared__ IpmState<T> Ss;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, N = d.N;
+    const int RG = PL::region(N), vec = PL::vec(N);
+    LdsT<T> *base = (LdsT<T> *)reinterpret_cast<T *>(dsmem);
+    auto region = [&](int v) { return base + (size_t)v * RG; };
+    auto lds_of = [&](LdsT<T> *R, int l) {
+        IpmLds<T> L;
+        L.ring = R + vec + (l >> 5) * SWEEP_LDS;
+        L.shl = R + vec + PL::RING;
+        L.red = (T *)(R + vec + PL::RING + PL::SH);
+        return L;
+    };
+    auto wts_of = [&](LdsT<T> *R) { return R + vec + PL::RING + PL::SH + PL::RED; };
+    auto cms_of = [&](LdsT<T> *R) { return (LdsT<uint8_t> *)(R + vec + PL::RING + PL::SH + PL::RED + PL::WTS); };
+    if (threadIdx.x == 0) {
+        flag[0] = flag[1] = 0;
+        rem = -1;
+    }
+    __syncthreads();
+    // one problem per wave
+    // the problem index is the same on every lane of the wave: as a uniform (scalar) value, every
+    // pointer derived from it stays in SGPRs (as a per-lane value the one-wave mode spilled 888 B per
+    // lane and ran 11% slower than k_qp_ipm<.., 64>)
+    const int slot = 2 * blockIdx.x + w;
+    const int b = __builtin_amdgcn_readfirstlane(slot < d.B ? order[slot] : -1);
+    if (b >= 0 && (!only_active || d.scp[b].active)) {
+        LdsT<T> *R = region(w);
+        Ctx<T, ROBOT> C{};
+        ctx_setup<T, ROBOT, 64>(d, b, C, wts_of(R), cms_of(R), floor_s, floor_l);
+        gsync<64, 128>();
+        C.vb = R;
+        const IpmLds<T> L = lds_of(R, lane);
+        IpmState<T> S = ipm_state0<T>();
+        ipm_start<T, ROBOT, 64, 128>(d, C, b);
+        ipm_loop<T, ROBOT, 64, 128>(d, C, b, S, L, max_iter, eps_abs, eps_rel, eta,
+                                    share ? (const volatile LdsT<int> *)(flag + (1 - w)) : nullptr);
+        if (S.yielded) {
+            if (lane == 0) {
+                Ss = S;
+                rem = w;
+            }
+        } else {
+            ipm_finish<T, ROBOT, 64>(d, C, b, S);
+        }
+    }
+    if (lane == 0) flag[w] = 1;   // this wave is free (a yielding wave's flag is never read again)
+    __syncthreads();              // the first s_barrier of either wave since the start
+    // the unfinished problem, if any, on both waves
+    const int r = rem;
+    if (r >= 0) {
+        const int b2 = __builtin_amdgcn_readfirstlane(order[2 * blockIdx.x + r]);
+        LdsT<T> *R = region(r);
+        Ctx<T, ROBOT> C{};
+        ctx_setup<T, ROBOT, 128>(d, b2, C, wts_of(R), cms_of(R), floor_s, floor_l);   // (the same values)
+        __syncthreads();
+        C.vb = R;
+        C.wxs = region(1 - r);
+        const IpmLds<T> L = lds_of(R, lane);
+        IpmState<T> S = Ss;
+        S.yielded = 0;
+        ipm_loop<T, ROBOT, 128, 128>(d, C, b2, S, L, max_iter, eps_abs, eps_rel, eta, nullptr);
+        ipm_finish<T, ROBOT, 128>(d, C, b2, S);
+    }
+    // covariance scan jobs of a deterministic batch, each wave on its own (as in k_qp_ipm<.., 64>)
+    if (d.scan_ctr) {
+        __syncthreads();   // the dynamic LDS is free from here on
+        LdsT<T> *R = region(w);
+        for (;;) {
+            int j = 0;
+            if (lane == 0) j = (int)atomicAdd(d.scan_ctr, 1u);
+            j = __shfl(j, 0, 64);
+            if (j >= d.B) break;
+            if (only_active && !d.scp[j].active) continue;
+            cov_scan_problem<T, ROBOT>(d, j, R);
+        }
+    }
+}
+
+// Pair order of k_qp_pair: problems sorted by the Newton steps of their previous QP (stable
+// counting sort over ORD_KEYS buckets; inactive problems count zero), slot 2j the j-th slowest,
+// slot 2j + 1 the j-th fastest (-1 past an odd batch).  One workgroup of 1024 threads, B <=
+// ORD_MAXB; deterministic (ranks inside a bucket by index).
+constexpr int ORD_KEYS = 16, ORD_MAXB = 8192;
+template <typename T> __global__ void __launch_bounds__(1024) k_qp_order(DevBuf<T> d, int only_active, int *order) {
+    __shared__ int cnt[ORD_KEYS][ORD_MAXB / 64], start[ORD_KEYS], sorted[ORD_MAXB];
+    const int B = d.B, nch = (B + 63) / 64, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    auto key = [&](int bb) -> int {
+        if (bb >= B) return -1;
+        if (only_active && !d.scp[bb].active) return 0;
+        const int it = d.qp_iters[bb];
+        return it < 0 ? 0 : (it >= ORD_KEYS ? ORD_KEYS - 1 : it);
+    };
+    for (int c = wv; c < nch; c += 16) {
+        const int k0 = key(64 * c + lane);
+        for (int k = 0; k < ORD_KEYS; ++k) {
+            const unsigned long long m = __ballot(k0 == k);
+            if (lane == 0) cnt[k][c] = __popcll(m);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < ORD_KEYS) {   // offsets of each chunk inside its bucket
+        int run = 0;
+        for (int c = 0; c < nch; ++c) {
+            const int t = cnt[threadIdx.x][c];
+            cnt[threadIdx.x][c] = run;
+            run += t;
+        }
+        start[threadIdx.x] = run;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {   // bucket starts
+        int run = 0;
+        for (int k = 0; k < ORD_KEYS; ++k) {
+            const int t = start[k];
+            start[k] = run;
+            run += t;
+        }
+    }
+    __syncthreads();
+    for (int c = wv; c < nch; c += 16) {
+        const int bb = 64 * c + lane, k0 = key(bb);
+        int rank = 0;
+        for (int k = 0; k < ORD_KEYS; ++k) {
+            const unsigned long long m = __ballot(k0 == k);
+            if (k0 == k) rank = __popcll(m & ((1ull << lane) - 1ull));
+        }
+        if (k0 >= 0) sorted[start[k0] + cnt[k0][c] + rank] = bb;
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < (B + 1) / 2; j += 1024) {
+        order[2 * j] = sorted[B - 1 - j];
+        order[2 * j + 1] = B - 1 - j != j ? sorted[j] : -1;
+    }
 }
 
 #define INST(T, R)                                                                       \
     template __global__ void k_qp_ipm<T, R, 64>(DevBuf<T>, int, int, T, T, T, T, T);     \
     template __global__ void k_qp_ipm<T, R, 128>(DevBuf<T>, int, int, T, T, T, T, T);    \
-    template __global__ void k_qp_ipm<T, R, 256>(DevBuf<T>, int, int, T, T, T, T, T);
+    template __global__ void k_qp_ipm<T, R, 256>(DevBuf<T>, int, int, T, T, T, T, T);    \
+    template __global__ void k_qp_pair<T, R>(DevBuf<T>, const int *, int, int, int, T, T, T, T, T);
 INST(double, 0)
 INST(double, 1)
 INST(float, 0)
 INST(float, 1)
 #undef INST
+template __global__ void k_qp_order<double>(DevBuf<double>, int, int *);
+template __global__ void k_qp_order<float>(DevBuf<float>, int, int *);
+
+// dynamic LDS of k_qp_pair (0: the batch is too large for k_qp_order)
+size_t ipm_pair_lds_bytes(int N, int prec_bytes) {
+    const size_t e = prec_bytes == 8 ? PairLds<double>::region(N) : PairLds<float>::region(N);
+    return 2 * e * prec_bytes;
+}
+int ipm_pair_max_batch() { return ORD_MAXB; }
 
 size_t ipm_lds_bytes(int N, int prec_bytes, int nt) {
     const size_t vec = (((size_t)(N + 2) * 9 + 7) & ~size_t(7));

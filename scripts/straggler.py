@@ -39,3 +39,22 @@ c = np.corrcoef(cyc)
 print('correlation of per-problem cycles between consecutive iterations:',
       ['%.2f' % c[i, i + 1] for i in range(K - 1)])
 print('decisions per iteration:', [np.bincount(d + 1, minlength=5).tolist() for d in dec])
+
+# Pairing model (a two-wave workgroup holding two problems, one per wave; when one finishes, both
+# waves finish the other at r x the one-wave time per step): launch time = max over pairs of
+# min + (max - min) * r, pairs from the previous iteration's cycles (slowest with fastest) or random.
+R = float(os.environ.get('PAIR_R', '0.61'))
+rng = np.random.default_rng(0)
+for i in range(1, K):
+    pred, act = cyc[i - 1], cyc[i]
+    o = np.argsort(pred)
+    sorted_pairs = [(o[j], o[B - 1 - j]) for j in range(B // 2)]
+    rp = rng.permutation(B)
+    rand_pairs = [(rp[2 * j], rp[2 * j + 1]) for j in range(B // 2)]
+    oracle_o = np.argsort(act)
+    oracle_pairs = [(oracle_o[j], oracle_o[B - 1 - j]) for j in range(B // 2)]
+    def t(pairs):
+        return max(min(act[a], act[b]) + abs(act[a] - act[b]) * R for a, b in pairs)
+    print('iter %d: single %.4g  sorted-by-prev %.4g (%.3f)  random %.4g (%.3f)  perfect %.4g (%.3f)' % (
+        i, act.max(), t(sorted_pairs), t(sorted_pairs) / act.max(), t(rand_pairs), t(rand_pairs) / act.max(),
+        t(oracle_pairs), t(oracle_pairs) / act.max()))
