@@ -2136,6 +2136,8 @@ __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT>
         // k_qp_pair: the partner wave has finished, so this problem continues on both waves
         if (yield && __builtin_amdgcn_readfirstlane(*yield)) { S.yielded = 1; break; }
         const bool init = (it == 0);
+        const int stall0 = stall;
+        const T mu_prev0 = mu_prev, prim_prev0 = prim_prev;
         Norms<T, ROBOT> nm{0, 0, 0, 0, 0, 0, 0, 0};
         for (int k = tid; k < K1; k += G) phase_residual<T, ROBOT>(C, k, nm);
         T mx[6] = {nm.prim, nm.dual, nm.comp, nm.sp, nm.sd, nm.lmax};
@@ -2171,6 +2173,21 @@ __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT>
             if (stall >= 3 && merit <= T(1e3)) { status = CMPC_QP_SOLVED_INACCURATE; break; }
         }
         if (it == max_iter) break;
+        // The partner may finish while this iteration runs (both problems start together, so it
+        // detects convergence in the same residual pass).  Nothing of the iterate changes before
+        // the update, so up to the S blocks the loop can still leave and let the two-wave loop
+        // redo the iteration from its top, with the stopping-test state it started from: at about
+        // 0.57 of the one-wave time per Newton step, redoing beats finishing the iteration alone
+        // while less than ~40% of it is done (residual 19%, Phi factors and w 10%, S blocks 4%).
+        auto leave = [&]() {
+            if (!(yield && __builtin_amdgcn_readfirstlane(*yield))) return false;
+            S.yielded = 1;
+            stall = stall0;
+            mu_prev = mu_prev0;
+            prim_prev = prim_prev0;
+            return true;
+        };
+        if (leave()) break;
         // ---- Phi factors and the predictor's particular solution (knot-local), then the S blocks
         // and the predictor's Schur right-hand side
         for (int k = tid; k < K1; k += G) {
@@ -2181,10 +2198,12 @@ __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT>
         }
         gsync<G, WG>();
         STAMP(1);
+        if (leave()) break;
         if (G > 64) add_wx<T, G>(C.vb, C.wxs, N);
         for (int k = tid; k < K1; k += G) phase_sblock<T, ROBOT>(C, k);
         gsync<G, WG>();
         STAMP(2);
+        if (leave()) break;
         // ---- factorization of S with the predictor's forward elimination fused in
 #ifdef CMPC_STAMPS
         unsigned long long *fst = d.stamps + (size_t)b * 16;
@@ -2441,7 +2460,8 @@ __global__ void __launch_bounds__(128, 1) k_qp_pair(DevBuf<T> d, const int *orde
                 rem = w;
             }
         } else {
-            ipm_finish<T, ROBOT, 64>(d, C, b, S);
+            if (lane == 0) flag[w] = 1;   // free: the partner may leave its loop while this wave
+            ipm_finish<T, ROBOT, 64>(d, C, b, S);   // writes the outputs (global memory only)
         }
     }
     if (lane == 0) flag[w] = 1;   // this wave is free (a yielding wave's flag is never read again)
@@ -2459,8 +2479,18 @@ __global__ void __launch_bounds__(128, 1) k_qp_pair(DevBuf<T> d, const int *orde
         const IpmLds<T> L = lds_of(R, lane);
         IpmState<T> S = Ss;
         S.yielded = 0;
+#ifdef CMPC_STAMPS
+        const unsigned long long tb0 = __builtin_amdgcn_s_memtime();
+        const int it0 = S.it;
+#endif
         ipm_loop<T, ROBOT, 128, 128>(d, C, b2, S, L, max_iter, eps_abs, eps_rel, eta, nullptr);
         ipm_finish<T, ROBOT, 128>(d, C, b2, S);
+#ifdef CMPC_STAMPS
+        if (threadIdx.x == 0) {   // slots 9, 10: cycles and Newton steps on both waves
+            d.stamps[(size_t)b2 * 16 + 9] = __builtin_amdgcn_s_memtime() - tb0;
+            d.stamps[(size_t)b2 * 16 + 10] = (unsigned long long)(S.it - it0);
+        }
+#endif
     }
     // covariance scan jobs of a deterministic batch, each wave on its own (as in k_qp_ipm<.., 64>)
     if (d.scan_ctr) {
