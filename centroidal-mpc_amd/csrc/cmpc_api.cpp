@@ -22,9 +22,9 @@ template <typename T, int R> __global__ void k_lin_knots(DevBuf<T>, int, int);
 template <typename T, int R> __global__ void k_cov_scan(DevBuf<T>, int);
 template <typename T, int R, bool FULL> __global__ void k_assemble(DevBuf<T>, int);
 template <typename T, int R, int NTT> __global__ void k_qp_ipm(DevBuf<T>, int, int, T, T, T, T, T);
-template <typename T, int R> __global__ void k_qp_pair(DevBuf<T>, const int *, int, int, int, T, T, T, T, T);
-template <typename T> __global__ void k_qp_order(DevBuf<T>, int, int *);
-size_t ipm_pair_lds_bytes(int N, int prec_bytes);
+template <typename T, int R, int P> __global__ void k_qp_group(DevBuf<T>, const int *, int, int, int, T, T, T, T, T);
+template <typename T> __global__ void k_qp_order(DevBuf<T>, int, int, int *);
+size_t ipm_group_lds_bytes(int N, int prec_bytes, int P);
 int ipm_pair_max_batch();
 template <typename T> __global__ void k_interpolate(DevBuf<T>, int, int, T *, T *);
 template <typename T, int R> __global__ void k_contact_plan(DevBuf<T>, const cmpc_gait *, const T *, uint8_t *, T *, T *);
@@ -115,21 +115,30 @@ int qp_waves(cmpc_handle h) {
     return (h->N + 1 > 64 && 2L * h->B <= 4L * h->n_cu) ? 2 : 1;
 }
 
-// Paired QP workgroups (k_qp_pair: two problems per two-wave workgroup, both waves on whichever
-// problem is still running once the other has finished) in place of one wave per problem, for fp64
-// batches, when two such workgroups fit a CU's LDS and the batch fits k_qp_order.  Same-box A/B
-// (profiles/r03c_pair_ab.log): metric config QP 2.93 -> 2.75 ms (327k -> 348k SCP it/s); BASELINE
-// C3 (fp32, two Newton steps, no tail to balance) 0.744 -> 0.752 ms, so fp32 keeps one wave per
-// problem.  CMPC_QP_PAIR=0 turns them off (diagnostic A/B).
-bool qp_paired(cmpc_handle h) {
-    if (qp_waves(h) != 1 || h->B < 2 || h->B > ipm_pair_max_batch() || h->prec != CMPC_PREC_F64) return false;
+// Grouped QP workgroups (k_qp_group: P problems per P-wave workgroup, one per wave, all P waves on
+// the last one once the others have finished) in place of one wave per problem, for fp64 batches
+// that fit k_qp_order: four problems per workgroup where the four-chain recurrence applies (N >= 40)
+// and four regions fit a CU's LDS, else two.  Same-box A/B (profiles/r03c_pair_ab.log): pairs took
+// the metric config's QP from 2.93 to 2.75 ms; BASELINE C3 (fp32, two Newton steps, no tail to
+// balance) 0.744 -> 0.752 ms, so fp32 keeps one wave per problem.  Diagnostics: CMPC_QP_PAIR=0
+// turns grouping off, =2 keeps the groups but never shares a problem; CMPC_QP_GROUP=2|4 forces the
+// group size.  Returns P, or 0 for one wave per problem.
+int qp_group(cmpc_handle h) {
+    if (qp_waves(h) != 1 || h->B < 2 || h->B > ipm_pair_max_batch() || h->prec != CMPC_PREC_F64) return 0;
     if (const char *e = std::getenv("CMPC_QP_PAIR"))
-        if (e[0] == '0') return false;
-    return 2 * ipm_pair_lds_bytes(h->N, h->esz()) + 1024 <= 160 * 1024;
+        if (e[0] == '0') return 0;
+    const size_t cap = 160 * 1024 - 1024;
+    int P = h->N >= 40 && ipm_group_lds_bytes(h->N, (int)h->esz(), 4) <= cap ? 4 : 2;
+    if (const char *e = std::getenv("CMPC_QP_GROUP")) {
+        if (e[0] == '2') P = 2;
+        if (e[0] == '4' && h->N >= 40) P = 4;
+    }
+    if (ipm_group_lds_bytes(h->N, (int)h->esz(), P) > cap) P = 2;
+    return ipm_group_lds_bytes(h->N, (int)h->esz(), P) <= cap ? P : 0;
 }
 
-// CMPC_QP_PAIR=2: paired workgroups whose waves never share a problem (diagnostic: the cost of the
-// pairing itself)
+// CMPC_QP_PAIR=2: grouped workgroups whose waves never share a problem (diagnostic: the cost of the
+// grouping itself)
 int qp_pair_share() {
     const char *e = std::getenv("CMPC_QP_PAIR");
     return e && e[0] == '2' ? 0 : 1;
@@ -238,19 +247,26 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
         // (N+2) x 9 Schur vector and the sweep rings in LDS, the Schur blocks in the workspace
         const int nt = 64 * qp_waves(h);
         const T eta = T(qp_step_fraction(h));
-        if (qp_paired(h)) {
-            const size_t lds = ipm_pair_lds_bytes(h->N, (int)sizeof(T));
-            HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_qp_pair<T, R>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        if (const int P = qp_group(h)) {
+            const size_t lds = ipm_group_lds_bytes(h->N, (int)sizeof(T), P);
+            const void *fn = P == 4 ? reinterpret_cast<const void *>(&k_qp_group<T, R, 4>)
+                                    : reinterpret_cast<const void *>(&k_qp_group<T, R, 2>);
+            HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
             if (h->scan_deferred) {   // the scans run in the QP's waves
                 HIPCHK(hipMemsetAsync(h->scan_ctr, 0, sizeof(unsigned), h->stream));
                 d.scan_ctr = (unsigned *)h->scan_ctr;
                 h->scan_deferred = false;
             }
-            hipLaunchKernelGGL((k_qp_order<T>), dim3(1), dim3(1024), 0, h->stream, d, only_active, (int *)h->qp_order);
-            hipLaunchKernelGGL((k_qp_pair<T, R>), dim3((unsigned)((B + 1) / 2)), dim3(128), lds, h->stream, d,
-                               (const int *)h->qp_order, only_active, qp_pair_share(), h->qs.max_iter, T(h->qs.eps_abs),
-                               T(h->qs.eps_rel), eta, T(h->qs.init_floor_s), T(h->qs.init_floor_l));
+            hipLaunchKernelGGL((k_qp_order<T>), dim3(1), dim3(1024), 0, h->stream, d, only_active, P, (int *)h->qp_order);
+            const unsigned ng = (unsigned)((B + P - 1) / P);
+            if (P == 4)
+                hipLaunchKernelGGL((k_qp_group<T, R, 4>), dim3(ng), dim3(256), lds, h->stream, d, (const int *)h->qp_order,
+                                   only_active, qp_pair_share(), h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), eta,
+                                   T(h->qs.init_floor_s), T(h->qs.init_floor_l));
+            else
+                hipLaunchKernelGGL((k_qp_group<T, R, 2>), dim3(ng), dim3(128), lds, h->stream, d, (const int *)h->qp_order,
+                                   only_active, qp_pair_share(), h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), eta,
+                                   T(h->qs.init_floor_s), T(h->qs.init_floor_l));
             if (h->scan_pending) {
                 HIPCHK(hipStreamWaitEvent(h->stream, h->ev_scan, 0));
                 h->scan_pending = false;
@@ -614,7 +630,7 @@ int cmpc_create(cmpc_handle *out, int device, int robot, int N, int max_batch, i
         HIPCHK(hipEventCreateWithFlags(&h->ev_pfK, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&h->ev_pfS, hipEventDisableTiming));
         h->scan_ctr = h->dalloc(16);
-        h->qp_order = h->dalloc(((size_t)max_batch + 1) * 4);
+        h->qp_order = h->dalloc(((size_t)max_batch + 8) * 4);   // ceil(B / P) P slots
         HIPCHK(hipDeviceGetAttribute(&h->n_cu, hipDeviceAttributeMultiprocessorCount, device));
         for (auto &e : h->ev) HIPCHK(hipEventCreate(&e));
         const size_t Bm = max_batch, K1 = N + 1, NB = N + 2, e = h->esz(), NC = h->NC;

@@ -39,7 +39,7 @@ struct cmpc_handle_s {
     bool scan_deferred = false, scan_pending = false;
     int scan_oa = 0;            // only_active of the deferred scan (settle_all)
     void *scan_ctr = nullptr;   // job counter of the scans run by the QP kernel's workgroups
-    void *qp_order = nullptr;   // (max_batch + 1) problem order of the paired QP kernel (k_qp_order)
+    void *qp_order = nullptr;   // (max_batch + 8) problem slots of the grouped QP kernel (k_qp_order)
     hipEvent_t ev[5] = {};
     bool timed = false;
     // accumulated timing: one 5-event record per cmpc_scp_iterate since cmpc_timing_reset

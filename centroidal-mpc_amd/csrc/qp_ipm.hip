@@ -2016,7 +2016,7 @@ __device__ __forceinline__ T refine_direction(const Ctx<T, ROBOT> &C, T sigma_mu
 }
 
 // ------------------------------------------------------------------ kernels
-// Newton-loop state of one problem's solve (carried across k_qp_pair's change of mode)
+// Newton-loop state of one problem's solve (carried across k_qp_group's change of mode)
 template <typename T> struct IpmState {
     int status, it, stall, n_refine, yielded;
     T mu_prev, merit, prim_prev;
@@ -2109,11 +2109,11 @@ __device__ __forceinline__ void ipm_start(const DevBuf<T> &d, const Ctx<T, ROBOT
 
 // Newton iterations of problem b on a group of G threads (the workgroup, or one wave of a WG-thread
 // workgroup), from S.it until the stopping test, a failure exit or the cap; with `yield` set, the
-// loop also leaves (S.yielded) at the top of an iteration once *yield is nonzero.
+// loop also leaves (S.yielded) once *yield (the workgroup's count of free waves) reaches yield_at.
 template <typename T, int ROBOT, int G, int WG>
 __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT> &C, int b, IpmState<T> &S,
                                          const IpmLds<T> &L, int max_iter, T eps_abs, T eps_rel, T eta,
-                                         const volatile LdsT<int> *yield) {
+                                         const volatile LdsT<int> *yield, int yield_at = 1) {
     const int tid = threadIdx.x & (G - 1), N = C.N, K1 = N + 1, NB = N + 2, NBm = NB / 2;
     (void)b;
 #ifdef CMPC_STAMPS
@@ -2133,8 +2133,8 @@ __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT>
     // equality-feasible least-squares start; s and lambda are then floored row by row (Solo12)
     // or shifted by 1 + the largest violation (TALOS), see init_s_knot.
     for (it = S.it; it <= max_iter; ++it) {
-        // k_qp_pair: the partner wave has finished, so this problem continues on both waves
-        if (yield && __builtin_amdgcn_readfirstlane(*yield)) { S.yielded = 1; break; }
+        // k_qp_group: the other waves have finished, so this problem continues on all of them
+        if (yield && __builtin_amdgcn_readfirstlane(*yield) >= yield_at) { S.yielded = 1; break; }
         const bool init = (it == 0);
         const int stall0 = stall;
         const T mu_prev0 = mu_prev, prim_prev0 = prim_prev;
@@ -2180,7 +2180,7 @@ __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT>
         // 0.57 of the one-wave time per Newton step, redoing beats finishing the iteration alone
         // while less than ~40% of it is done (residual 19%, Phi factors and w 10%, S blocks 4%).
         auto leave = [&]() {
-            if (!(yield && __builtin_amdgcn_readfirstlane(*yield))) return false;
+            if (!(yield && __builtin_amdgcn_readfirstlane(*yield) >= yield_at)) return false;
             S.yielded = 1;
             stall = stall0;
             mu_prev = mu_prev0;
@@ -2214,7 +2214,7 @@ __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT>
 #ifdef CMPC_STAMPS
             const unsigned long long tc0 = __builtin_amdgcn_s_memtime();
 #endif
-            pt_factor_chains<T>(C.Sd, C.So, C.Sh, C.Sx, NB, C.sp, L.shl + (tid >> 6) * PT_SCRATCH, C.vb, C.sbv);
+            pt_factor_chains<T>(C.Sd, C.So, C.Sh, C.Sx, NB, C.sp, L.shl, C.vb, C.sbv);   // (this wave's scratch)
 #ifdef CMPC_STAMPS
             const unsigned long long tc1 = __builtin_amdgcn_s_memtime();
 #endif
@@ -2356,7 +2356,9 @@ __global__ void __launch_bounds__(NTT, NTT == 128 ? QP_MIN_WAVES_2W : QP_MIN_WAV
     const int vec = (NB * 9 + 7) & ~7;
     IpmLds<T> L;
     L.ring = C.vb + vec + (NTT >= 256 ? (tid >> 6) : ((tid & 63) >> 5)) * SWEEP_LDS;
-    L.shl = (LdsT<T> *)sh;
+    // recurrence scratch: the two ends' (two-ended kernels), this wave's (four chains; pt_reduced
+    // runs on wave 0, whose block is the first)
+    L.shl = (LdsT<T> *)sh + (NTT >= 256 ? (tid >> 6) * PT_SCRATCH : 0);
     L.red = red;
     if (NTT > 64) C.wxs = C.vb + vec + NRING * SWEEP_LDS;
     if (NTT >= 256) {
@@ -2391,102 +2393,118 @@ __global__ void __launch_bounds__(NTT, NTT == 128 ? QP_MIN_WAVES_2W : QP_MIN_WAV
     }
 }
 
-// ------------------------------------------------------------------ paired problems
+// ------------------------------------------------------------------ grouped problems
 // Batches of one wave per problem (the metric config: 1024 problems, one per SIMD) last as long as
 // their slowest problem: trot N=100 x 1024 takes 4 to 7 Newton steps per problem, so the SIMD of a
-// 4-step problem idles for three steps.  k_qp_pair holds two problems per two-wave workgroup,
-// one per wave (the one-wave algorithm, ipm_loop<.., 64, 128>); once one of them has finished, the
-// other leaves its loop at the top of its next iteration and both waves finish it with the
-// two-wave algorithm (ipm_loop<.., 128, 128>: one knot per thread, one end of the Schur
-// recurrence per wave).  k_qp_order pairs the problems that took the most Newton steps in the
-// previous QP launch with those that took the fewest (inactive problems count zero).
+// 4-step problem idles for three steps.  k_qp_group holds P problems per P-wave workgroup, one per
+// wave (the one-wave algorithm, ipm_loop<.., 64, 64 P>); once all but one have finished, the last
+// one leaves its loop (at the top of an iteration, or redoing the current one) and all P waves
+// finish it: with the two-wave algorithm (P = 2: one knot per thread, one end of the Schur
+// recurrence per wave) or the four-wave one (P = 4: four chains around three separators,
+// schur_pt.hpp).  k_qp_order puts the problems that took the most Newton steps in the previous
+// launch with those that took the fewest (inactive problems count zero).
 //
 // LDS of one wave's problem (elements of T): Schur vector | two sweep rings (the two halves of
-// the wave) | recurrence scratch of the two ends | reductions | cost weights | contact masks.  In
-// the two-wave mode the remaining problem keeps its region, and the other one's Schur-vector slot
-// holds the w_x side array (add_wx).
-template <typename T> struct PairLds {
-    static constexpr int RING = 2 * SWEEP_LDS, SH = 2 * TW_SCRATCH, RED = 16, WTS = 48;
+// the wave) | recurrence scratch of the two ends | reductions | cost weights | contact masks.  When
+// all waves finish the last problem, it keeps its region; the other regions hold the w_x side
+// array and (P = 4) the fill products in their Schur-vector slots, and each wave uses its own
+// region's first ring and recurrence scratch.
+template <typename T> struct GroupLds {
+    static constexpr int RING = 2 * SWEEP_LDS, SH = 2 * TW_SCRATCH, RED = 32, WTS = 48;
     static constexpr int CMS = (KPC + 8 * (int)sizeof(T) - 1) / (8 * (int)sizeof(T)) * 8;
+    static_assert(SH >= PT_SCRATCH, "a region holds one wave's four-chain scratch");
     __host__ __device__ static constexpr int vec(int N) { return ((N + 2) * 9 + 7) & ~7; }
     __host__ __device__ static constexpr int region(int N) { return vec(N) + RING + SH + RED + WTS + CMS; }
 };
 
-template <typename T, int ROBOT>
-__global__ void __launch_bounds__(128, 1) k_qp_pair(DevBuf<T> d, const int *order, int only_active, int share,
-                                                    int max_iter, T eps_abs, T eps_rel, T eta, T floor_s, T floor_l) {
+template <typename T, int ROBOT, int P>
+__global__ void __launch_bounds__(64 * P, 1) k_qp_group(DevBuf<T> d, const int *order, int only_active, int share,
+                                                        int max_iter, T eps_abs, T eps_rel, T eta, T floor_s,
+                                                        T floor_l) {
     extern __shared__ __attribute__((aligned(16))) unsigned char dsmem[];
-    using PL = PairLds<T>;
-    __shared__ int flag[2], rem;
+    using GL = GroupLds<T>;
+    constexpr int WG = 64 * P;
+    __shared__ int nfree, rem;
     __shared__ IpmState<T> Ss;
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, N = d.N;
-    const int RG = PL::region(N), vec = PL::vec(N);
+    __shared__ T sbv_s[P >= 4 ? 6 * 9 : 1];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, N = d.N, NB = N + 2;
+    const int RG = GL::region(N), vec = GL::vec(N);
     LdsT<T> *base = (LdsT<T> *)reinterpret_cast<T *>(dsmem);
     auto region = [&](int v) { return base + (size_t)v * RG; };
-    auto lds_of = [&](LdsT<T> *R, int l) {
-        IpmLds<T> L;
-        L.ring = R + vec + (l >> 5) * SWEEP_LDS;
-        L.shl = R + vec + PL::RING;
-        L.red = (T *)(R + vec + PL::RING + PL::SH);
-        return L;
-    };
-    auto wts_of = [&](LdsT<T> *R) { return R + vec + PL::RING + PL::SH + PL::RED; };
-    auto cms_of = [&](LdsT<T> *R) { return (LdsT<uint8_t> *)(R + vec + PL::RING + PL::SH + PL::RED + PL::WTS); };
+    auto wts_of = [&](LdsT<T> *R) { return R + vec + GL::RING + GL::SH + GL::RED; };
+    auto cms_of = [&](LdsT<T> *R) { return (LdsT<uint8_t> *)(R + vec + GL::RING + GL::SH + GL::RED + GL::WTS); };
     if (threadIdx.x == 0) {
-        flag[0] = flag[1] = 0;
+        nfree = 0;
         rem = -1;
     }
     __syncthreads();
-    // one problem per wave
-    // the problem index is the same on every lane of the wave: as a uniform (scalar) value, every
-    // pointer derived from it stays in SGPRs (as a per-lane value the one-wave mode spilled 888 B per
-    // lane and ran 11% slower than k_qp_ipm<.., 64>)
-    const int slot = 2 * blockIdx.x + w;
+    // one problem per wave.  The problem index is the same on every lane of the wave: as a uniform
+    // (scalar) value, every pointer derived from it stays in SGPRs (as a per-lane value the one-wave
+    // mode spilled 888 B per lane and ran 11% slower than k_qp_ipm<.., 64>)
+    const int slot = P * blockIdx.x + w;
     const int b = __builtin_amdgcn_readfirstlane(slot < d.B ? order[slot] : -1);
     if (b >= 0 && (!only_active || d.scp[b].active)) {
         LdsT<T> *R = region(w);
         Ctx<T, ROBOT> C{};
         ctx_setup<T, ROBOT, 64>(d, b, C, wts_of(R), cms_of(R), floor_s, floor_l);
-        gsync<64, 128>();
+        gsync<64, WG>();
         C.vb = R;
-        const IpmLds<T> L = lds_of(R, lane);
+        IpmLds<T> L;
+        L.ring = R + vec + (lane >> 5) * SWEEP_LDS;
+        L.shl = R + vec + GL::RING;
+        L.red = (T *)(R + vec + GL::RING + GL::SH);
         IpmState<T> S = ipm_state0<T>();
-        ipm_start<T, ROBOT, 64, 128>(d, C, b);
-        ipm_loop<T, ROBOT, 64, 128>(d, C, b, S, L, max_iter, eps_abs, eps_rel, eta,
-                                    share ? (const volatile LdsT<int> *)(flag + (1 - w)) : nullptr);
+        ipm_start<T, ROBOT, 64, WG>(d, C, b);
+        ipm_loop<T, ROBOT, 64, WG>(d, C, b, S, L, max_iter, eps_abs, eps_rel, eta,
+                                   share ? (const volatile LdsT<int> *)&nfree : nullptr, P - 1);
         if (S.yielded) {
             if (lane == 0) {
                 Ss = S;
                 rem = w;
             }
         } else {
-            if (lane == 0) flag[w] = 1;   // free: the partner may leave its loop while this wave
-            ipm_finish<T, ROBOT, 64>(d, C, b, S);   // writes the outputs (global memory only)
+            if (lane == 0) atomicAdd(&nfree, 1);   // free: the last problem may leave its loop while
+            ipm_finish<T, ROBOT, 64>(d, C, b, S);  // this wave writes the outputs (global memory only)
         }
+    } else if (lane == 0) {
+        atomicAdd(&nfree, 1);
     }
-    if (lane == 0) flag[w] = 1;   // this wave is free (a yielding wave's flag is never read again)
-    __syncthreads();              // the first s_barrier of either wave since the start
-    // the unfinished problem, if any, on both waves
+    __syncthreads();   // the first s_barrier of any wave since the start
+    // the last problem, if it left its loop, on all waves
     const int r = rem;
     if (r >= 0) {
-        const int b2 = __builtin_amdgcn_readfirstlane(order[2 * blockIdx.x + r]);
+        const int b2 = __builtin_amdgcn_readfirstlane(order[P * blockIdx.x + r]);
         LdsT<T> *R = region(r);
         Ctx<T, ROBOT> C{};
-        ctx_setup<T, ROBOT, 128>(d, b2, C, wts_of(R), cms_of(R), floor_s, floor_l);   // (the same values)
+        ctx_setup<T, ROBOT, WG>(d, b2, C, wts_of(R), cms_of(R), floor_s, floor_l);   // (the same values)
         __syncthreads();
         C.vb = R;
-        C.wxs = region(1 - r);
-        const IpmLds<T> L = lds_of(R, lane);
+        C.wxs = region((r + 1) % P);
+        LdsT<T> *Rw = region(w);   // this wave's region: its first ring and recurrence scratch
+        IpmLds<T> L;
+        if constexpr (P >= 4) {
+            C.Sh = C.ws + Ws<ROBOT>::Sh;
+            C.Sx = C.ws + Ws<ROBOT>::Sx;
+            pt_seps<T>(NB, C.sp);
+            C.sbv = (LdsT<T> *)sbv_s;
+            C.hy = region((r + 2) % P);
+            L.ring = Rw + vec;
+            L.shl = Rw + vec + GL::RING;
+        } else {   // the two ends' sweeps run on the halves of wave 0; the ends' scratch is R's
+            L.ring = R + vec + (lane >> 5) * SWEEP_LDS;
+            L.shl = R + vec + GL::RING;
+        }
+        L.red = (T *)(R + vec + GL::RING + GL::SH);
         IpmState<T> S = Ss;
         S.yielded = 0;
 #ifdef CMPC_STAMPS
         const unsigned long long tb0 = __builtin_amdgcn_s_memtime();
         const int it0 = S.it;
 #endif
-        ipm_loop<T, ROBOT, 128, 128>(d, C, b2, S, L, max_iter, eps_abs, eps_rel, eta, nullptr);
-        ipm_finish<T, ROBOT, 128>(d, C, b2, S);
+        ipm_loop<T, ROBOT, WG, WG>(d, C, b2, S, L, max_iter, eps_abs, eps_rel, eta, nullptr);
+        ipm_finish<T, ROBOT, WG>(d, C, b2, S);
 #ifdef CMPC_STAMPS
-        if (threadIdx.x == 0) {   // slots 9, 10: cycles and Newton steps on both waves
+        if (threadIdx.x == 0) {   // slots 9, 10: cycles and Newton steps on all waves
             d.stamps[(size_t)b2 * 16 + 9] = __builtin_amdgcn_s_memtime() - tb0;
             d.stamps[(size_t)b2 * 16 + 10] = (unsigned long long)(S.it - it0);
         }
@@ -2507,12 +2525,13 @@ __global__ void __launch_bounds__(128, 1) k_qp_pair(DevBuf<T> d, const int *orde
     }
 }
 
-// Pair order of k_qp_pair: problems sorted by the Newton steps of their previous QP (stable
-// counting sort over ORD_KEYS buckets; inactive problems count zero), slot 2j the j-th slowest,
-// slot 2j + 1 the j-th fastest (-1 past an odd batch).  One workgroup of 1024 threads, B <=
-// ORD_MAXB; deterministic (ranks inside a bucket by index).
+// Group order of k_qp_group: problems sorted by the Newton steps of their previous QP (stable
+// counting sort over ORD_KEYS buckets; inactive problems count zero).  With ng = ceil(B / P)
+// groups, slot P g holds the g-th slowest problem and slots P g + 1 .. P g + P - 1 the fastest
+// remaining ones in order (-1 once they run out).  One workgroup of 1024 threads, B <= ORD_MAXB;
+// deterministic (ranks inside a bucket by index).
 constexpr int ORD_KEYS = 16, ORD_MAXB = 8192;
-template <typename T> __global__ void __launch_bounds__(1024) k_qp_order(DevBuf<T> d, int only_active, int *order) {
+template <typename T> __global__ void __launch_bounds__(1024) k_qp_order(DevBuf<T> d, int only_active, int P, int *order) {
     __shared__ int cnt[ORD_KEYS][ORD_MAXB / 64], start[ORD_KEYS], sorted[ORD_MAXB];
     const int B = d.B, nch = (B + 63) / 64, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     auto key = [&](int bb) -> int {
@@ -2558,9 +2577,15 @@ template <typename T> __global__ void __launch_bounds__(1024) k_qp_order(DevBuf<
         if (k0 >= 0) sorted[start[k0] + cnt[k0][c] + rank] = bb;
     }
     __syncthreads();
-    for (int j = threadIdx.x; j < (B + 1) / 2; j += 1024) {
-        order[2 * j] = sorted[B - 1 - j];
-        order[2 * j + 1] = B - 1 - j != j ? sorted[j] : -1;
+    const int ng = (B + P - 1) / P, nfast = B - ng;
+    for (int t = threadIdx.x; t < ng * P; t += 1024) {
+        const int g = t / P, q = t % P;
+        if (q == 0) {
+            order[t] = sorted[B - 1 - g];
+        } else {
+            const int f = g * (P - 1) + q - 1;
+            order[t] = f < nfast ? sorted[f] : -1;
+        }
     }
 }
 
@@ -2568,19 +2593,20 @@ template <typename T> __global__ void __launch_bounds__(1024) k_qp_order(DevBuf<
     template __global__ void k_qp_ipm<T, R, 64>(DevBuf<T>, int, int, T, T, T, T, T);     \
     template __global__ void k_qp_ipm<T, R, 128>(DevBuf<T>, int, int, T, T, T, T, T);    \
     template __global__ void k_qp_ipm<T, R, 256>(DevBuf<T>, int, int, T, T, T, T, T);    \
-    template __global__ void k_qp_pair<T, R>(DevBuf<T>, const int *, int, int, int, T, T, T, T, T);
+    template __global__ void k_qp_group<T, R, 2>(DevBuf<T>, const int *, int, int, int, T, T, T, T, T); \
+    template __global__ void k_qp_group<T, R, 4>(DevBuf<T>, const int *, int, int, int, T, T, T, T, T);
 INST(double, 0)
 INST(double, 1)
 INST(float, 0)
 INST(float, 1)
 #undef INST
-template __global__ void k_qp_order<double>(DevBuf<double>, int, int *);
-template __global__ void k_qp_order<float>(DevBuf<float>, int, int *);
+template __global__ void k_qp_order<double>(DevBuf<double>, int, int, int *);
+template __global__ void k_qp_order<float>(DevBuf<float>, int, int, int *);
 
-// dynamic LDS of k_qp_pair (0: the batch is too large for k_qp_order)
-size_t ipm_pair_lds_bytes(int N, int prec_bytes) {
-    const size_t e = prec_bytes == 8 ? PairLds<double>::region(N) : PairLds<float>::region(N);
-    return 2 * e * prec_bytes;
+// dynamic LDS of k_qp_group with P problems per workgroup
+size_t ipm_group_lds_bytes(int N, int prec_bytes, int P) {
+    const size_t e = prec_bytes == 8 ? GroupLds<double>::region(N) : GroupLds<float>::region(N);
+    return (size_t)P * e * prec_bytes;
 }
 int ipm_pair_max_batch() { return ORD_MAXB; }
 

@@ -8,11 +8,3 @@ timeout -k 10 700 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-me
 tail -2 gpurun_out/pytest_gpu.log
 timeout -k 10 300 python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/bench_q.json 2> gpurun_out/bench_q.err || { tail -20 gpurun_out/bench_q.err; exit 1; }
 cat gpurun_out/bench_q.json
-# two-wave kernel at two waves per SIMD (variant w2) against the default on the metric config
-for v in a b; do
-  timeout -k 10 200 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-extras > gpurun_out/w2_def_$v.json 2>&1 || exit 1
-  CMPC_QP_WAVES=2 CMPC_LIB_VARIANT=w2 timeout -k 10 200 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-extras > gpurun_out/w2_var_$v.json 2>&1 || exit 1
-done
-CMPC_QP_WAVES=2 timeout -k 10 200 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-extras > gpurun_out/w2_def2w.json 2>&1 || exit 1
-for f in gpurun_out/w2_*.json; do python3 -c "
-import json,sys; d=json.loads(open('$f').read().strip().splitlines()[-1]); print('$f', round(d['value']), d['phase_ms_per_step'])"; done
