@@ -424,7 +424,10 @@ template <int n, typename T, typename P> __device__ __forceinline__ void stv(P p
 // the fp32 floor on Solo12 trot came from the dual scale, see the multiplier term below).
 template <typename T> struct Acc { using type = T; };
 
-template <typename T, int ROBOT>
+// PART (four-wave workgroups with one pass of knots, split_knots): -1 the whole knot; 0 the state
+// part (dynamics and boundary rows, trust-region and slack rows, r_dx, r_dt); 1 the contact part
+// (friction / CoP rows, r_du).  The norms of both parts meet in the block reduction.
+template <typename T, int ROBOT, int PART = -1>
 __device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<T, ROBOT> &nm, const T *__restrict__ stp,
                                            const T *__restrict__ xs, const T *__restrict__ us, const T *__restrict__ ts,
                                            const T *__restrict__ ss, const T *__restrict__ ls, const T *__restrict__ nus,
@@ -448,7 +451,7 @@ __device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<
         nk[i] = nus[i * ld];      // nu blocks k, k + 1
         n1[i] = nus[i * ld + 1];
     }
-    if (sizeof(T) == 4) {
+    if (sizeof(T) == 4 && PART != 1) {
         // fp32: the dual scale also counts the multipliers the rows sum.  E' nu = -nu_k + A_k' nu_{k+1}
         // cancels (Solo12 trot: |nu| ~ 1e5 against |E' nu| ~ 2e3), and |nu| in fp32 alone carries
         // ~6e-8 |nu| of rounding into every dual row: without this term the 1e-6 relative test sat
@@ -466,11 +469,12 @@ __device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<
     A ex[9], eu[NU];
     for (int i = 0; i < 9; ++i) ex[i] = (k == 0) ? nk[i] : -nk[i];
     if (k == N) for (int i = 0; i < 9; ++i) ex[i] += n1[i];
-    if (hu) {
+    if (hu && PART == 1) opBT<A, ROBOT>(st, n1, eu);
+    if (hu && PART != 1) {
         A a[9];
         opAT(w, beta, n1, a);
         for (int i = 0; i < 9; ++i) ex[i] += a[i];
-        opBT<A, ROBOT>(st, n1, eu);
+        if (PART != 0) opBT<A, ROBOT>(st, n1, eu);
         // dynamics row block 1 + k first: its loads (x_{k+1}, r_k) are then dead before the rows
         A ax[9], bu[9];
         opA(w, beta, x, ax);
@@ -484,7 +488,7 @@ __device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<
             nm.sp = fmax(nm.sp, T(fmax(fabs(ez), fabs(r))));
         }
     }
-    if (k == 0 || k == N) {   // boundary rows: block 0 (initial state) / N + 1 (final state)
+    if (PART != 1 && (k == 0 || k == N)) {   // boundary rows: block 0 (initial state) / N + 1 (final state)
         const T *xb = C.xbar + (size_t)k * 9;
         for (int i = 0; i < 9; ++i) {
             const A rb = x[i] - A(xb[i]);
@@ -511,18 +515,20 @@ __device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<
         nm.lmax = fmax(nm.lmax, pr ? T(lr) : T(0));
         return pr ? lr : A(0);
     };
-    nm.cnt += T(9 + (hu ? 4 * (1 + Robot<ROBOT>::COP) * __builtin_popcount(msk) : 0));
+    nm.cnt += T((PART != 1 ? 9 : 0) + (hu && PART != 0 ? 4 * (1 + Robot<ROBOT>::COP) * __builtin_popcount(msk) : 0));
+    if (PART != 1) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const A g = tr_sign<A>(j, 0) * x[6] + tr_sign<A>(j, 1) * x[7] + tr_sign<A>(j, 2) * x[8] + cw * t;
-        const A lr = row(j, true, g, st[S::BTR + j]);
-        for (int i = 0; i < 3; ++i) gL[i] += tr_sign<A>(j, i) * lr;
-        gt += cw * lr;
+        for (int j = 0; j < 8; ++j) {
+            const A g = tr_sign<A>(j, 0) * x[6] + tr_sign<A>(j, 1) * x[7] + tr_sign<A>(j, 2) * x[8] + cw * t;
+            const A lr = row(j, true, g, st[S::BTR + j]);
+            for (int i = 0; i < 3; ++i) gL[i] += tr_sign<A>(j, i) * lr;
+            gt += cw * lr;
+        }
+        gt -= row(8, true, -t, A(0));
+        nm.mu += mug;
     }
-    gt -= row(8, true, -t, A(0));
-    nm.mu += mug;
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
+    for (int c = 0; c < (PART != 0 ? NC : 0); ++c) {
         mug = T(0);
         const bool pr = hu && ((msk >> c) & 1u);
         const auto cs = st + (S::CON + S::CS * c);
@@ -547,6 +553,7 @@ __device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<
         }
         nm.mu += mug;
     }
+    if (PART != 1) {
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
         const A hx = A(C.Wx(i)) * x[i], q = st[S::QX + i];
@@ -560,7 +567,8 @@ __device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<
     rdt_o[0] = T(rdt);
     nm.dual = fmax(nm.dual, T(fabs(rdt)));
     nm.sd = fmax(nm.sd, T(1));
-    if (hu) {
+    }
+    if (hu && PART != 0) {
 #pragma unroll
         for (int i = 0; i < NU; ++i) {
             const A h = A(C.Wu(i)) * u[i];
@@ -572,9 +580,9 @@ __device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<
     }
 }
 
-template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_residual(const Ctx<T, ROBOT> &C, int k, Norms<T, ROBOT> &nm) {
+template <typename T, int ROBOT, int PART = -1> __device__ PHASE_ATTR void phase_residual(const Ctx<T, ROBOT> &C, int k, Norms<T, ROBOT> &nm) {
     T *ws = C.ws;
-    resid_knot<T, ROBOT>(C, k, nm, C.stage + k, ws + WF(x) * KPC + k, ws + WF(u) * KPC + k, ws + WF(t) * KPC + k,
+    resid_knot<T, ROBOT, PART>(C, k, nm, C.stage + k, ws + WF(x) * KPC + k, ws + WF(u) * KPC + k, ws + WF(t) * KPC + k,
                          ws + WF(s) * KPC + k, ws + WF(l) * KPC + k, ws + WF(nu) * KPC + k, ws + WF(rdx) * KPC + k,
                          ws + WF(rdt) * KPC + k, ws + WF(rdu) * KPC + k, ws + WF(rde) * KPC, ws + WF(rdi) * KPC + k);
 }
@@ -1577,7 +1585,9 @@ template <typename T, int ROBOT> __device__ __forceinline__ void phase_w_pred(co
 // steps.
 // ACC (refinement): the solve gives the correction of the corrector direction; the stored
 // direction becomes direction + correction and the ratio test runs on the sum.
-template <typename T, int ROBOT, bool ACC = false>
+// PART as in resid_knot: 0 the (x, t) part and the trust-region / slack rows, 1 the controls and
+// the contact rows (-1 both)
+template <typename T, int ROBOT, bool ACC = false, int PART = -1>
 __device__ __forceinline__ T dz_knot(const Ctx<T, ROBOT> &C, int k, T (&mus)[3], bool prod, const T *__restrict__ stp,
                                      const T *__restrict__ rhp, const T *__restrict__ rdxp, const T *__restrict__ rdtp,
                                      const T *__restrict__ wup, const T *__restrict__ ss, const T *__restrict__ ls,
@@ -1598,10 +1608,12 @@ __device__ __forceinline__ T dz_knot(const Ctx<T, ROBOT> &C, int k, T (&mus)[3],
     T dk[9], d1[9], ex[9], eu[NU], a[9], w[3];
     for (int i = 0; i < 9; ++i) { dk[i] = vb[k * 9 + i]; d1[i] = vb[(k + 1) * 9 + i]; }
     for (int i = 0; i < 3; ++i) w[i] = st[S::W + i];
-    opAT(w, C.beta, d1, a);
-    opBT<T, ROBOT>(st, d1, eu);
-    for (int i = 0; i < 9; ++i)
-        ex[i] = (k == 0 ? dk[i] : -dk[i]) + (hu ? a[i] : T(0)) + (k == N ? d1[i] : T(0));
+    if (PART != 1) {
+        opAT(w, C.beta, d1, a);
+        for (int i = 0; i < 9; ++i)
+            ex[i] = (k == 0 ? dk[i] : -dk[i]) + (hu ? a[i] : T(0)) + (k == N ? d1[i] : T(0));
+    }
+    if (PART != 0) opBT<T, ROBOT>(st, d1, eu);
     T amax = T(1);
     // stores: corrector ds, dl; predictor ds_aff dl_aff in the ds field (the corrector's r_hat
     // term) or, in the initialization step (whose full step is the affine one), ds_aff itself
@@ -1622,9 +1634,9 @@ __device__ __forceinline__ T dz_knot(const Ctx<T, ROBOT> &C, int k, T (&mus)[3],
     // their use were each waited on alone)
     T wuv[NU], rduv[NU];
 #pragma unroll
-    for (int q = 0; q < NU; ++q) { wuv[q] = wup[q * ld]; rduv[q] = rdup[q * ld]; }
+    for (int q = 0; q < (PART != 0 ? NU : 0); ++q) { wuv[q] = wup[q * ld]; rduv[q] = rdup[q * ld]; }
     // (x, t) part and the trust-region / slack rows
-    {
+    if (PART != 1) {
         T rdx[9], s9[9], l9[9], rh9[9], ri9[9];
 #pragma unroll
         for (int i = 0; i < 9; ++i) {
@@ -1655,7 +1667,7 @@ __device__ __forceinline__ T dz_knot(const Ctx<T, ROBOT> &C, int k, T (&mus)[3],
     }
     // contacts, one at a time: du = -w_u - Phi_u^-1 E'dnu_u, then the contact's rows
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
+    for (int c = 0; c < (PART != 0 ? NC : 0); ++c) {
         const bool pr = hu && ((msk >> c) & 1u);
         const auto cs = st + (S::CON + S::CS * c);
         T G[12], s4[4], l4[4], rh4[4], ri4[4], vf[3];
@@ -1705,11 +1717,11 @@ __device__ __forceinline__ T dz_knot(const Ctx<T, ROBOT> &C, int k, T (&mus)[3],
     return amax;
 }
 
-template <typename T, int ROBOT>
+template <typename T, int ROBOT, int PART = -1>
 __device__ PHASE_ATTR T phase_dz(const Ctx<T, ROBOT> &C, int k, int corr, bool init, T (&mus)[3]) {
     const int kc = k < C.N ? k : 0;   // k = N: no controls or contacts
     T *ws = C.ws;
-    return dz_knot<T, ROBOT>(C, k, mus, !corr && !init, C.stage + kc, ws + WF(rh) * KPC + k, ws + WF(rdx) * KPC + k,
+    return dz_knot<T, ROBOT, false, PART>(C, k, mus, !corr && !init, C.stage + kc, ws + WF(rh) * KPC + k, ws + WF(rdx) * KPC + k,
                              ws + WF(rdt) * KPC + k, ws + WF(wu) * KPC + kc, ws + WF(s) * KPC + k,
                              ws + WF(l) * KPC + k, ws + WF(rdi) * KPC + k, ws + WF(rdu) * KPC + kc,
                              ws + WF(dx) * KPC + k, ws + WF(dt) * KPC + k,
@@ -2016,6 +2028,11 @@ __device__ __forceinline__ T refine_direction(const Ctx<T, ROBOT> &C, T sigma_mu
 }
 
 // ------------------------------------------------------------------ kernels
+// Four-wave groups: the per-knot phases use only the first two waves at one knot per thread (up to
+// 128 knots), and their time is one knot's instruction stream, so the heaviest ones (residual,
+// direction) split each knot into a state part (waves 0, 1) and a contact part (waves 2, 3).
+template <int G> constexpr bool split_knots() { return G >= 256; }
+
 // Newton-loop state of one problem's solve (carried across k_qp_group's change of mode)
 template <typename T> struct IpmState {
     int status, it, stall, n_refine, yielded;
@@ -2139,7 +2156,16 @@ __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT>
         const int stall0 = stall;
         const T mu_prev0 = mu_prev, prim_prev0 = prim_prev;
         Norms<T, ROBOT> nm{0, 0, 0, 0, 0, 0, 0, 0};
-        for (int k = tid; k < K1; k += G) phase_residual<T, ROBOT>(C, k, nm);
+        if constexpr (split_knots<G>()) {   // a thread pair per knot: state part | contact part
+            // (the part is the wave's: a uniform branch)
+            if (__builtin_amdgcn_readfirstlane(tid) < 128) {
+                for (int k = tid & 127; k < K1; k += 128) phase_residual<T, ROBOT, 0>(C, k, nm);
+            } else {
+                for (int k = tid & 127; k < K1; k += 128) phase_residual<T, ROBOT, 1>(C, k, nm);
+            }
+        } else {
+            for (int k = tid; k < K1; k += G) phase_residual<T, ROBOT>(C, k, nm);
+        }
         T mx[6] = {nm.prim, nm.dual, nm.comp, nm.sp, nm.sd, nm.lmax};
         block_reduce<T, G, 6, 1, WG>(mx, L.red);
         T sm2[2] = {nm.mu, nm.cnt};
@@ -2257,7 +2283,15 @@ __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT>
             schur_backward<T, G, WG>(C, NB, NBm, L.ring);
             STAMP(6);
             T am[1] = {T(1)}, mus[3] = {T(0), T(0), T(0)};
-            for (int k = tid; k < K1; k += G) am[0] = fmin(am[0], phase_dz<T, ROBOT>(C, k, corr, init, mus));
+            if constexpr (split_knots<G>()) {
+                if (__builtin_amdgcn_readfirstlane(tid) < 128) {
+                    for (int k = tid & 127; k < K1; k += 128) am[0] = fmin(am[0], phase_dz<T, ROBOT, 0>(C, k, corr, init, mus));
+                } else {
+                    for (int k = tid & 127; k < K1; k += 128) am[0] = fmin(am[0], phase_dz<T, ROBOT, 1>(C, k, corr, init, mus));
+                }
+            } else {
+                for (int k = tid; k < K1; k += G) am[0] = fmin(am[0], phase_dz<T, ROBOT>(C, k, corr, init, mus));
+            }
             block_reduce<T, G, 1, 2, WG>(am, L.red);
             STAMP(7);
             alpha = am[0];
