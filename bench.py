@@ -304,7 +304,7 @@ def main():
         'qp_exit': {'status_counts': {str(int(a)): int(b) for a, b in zip(u, c)},
                     'merit_max': float(merit.max()), 'refined_problems': int((nref > 0).sum()),
                     'refine_steps': int(nref.sum())},
-        'roofline': {'kernel': 'k_qp_ipm', 'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
+        'roofline': {'kernel': solver.qp_kernel(), 'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                      'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
                      'compulsory': {'achieved': compulsory, 'frac': compulsory / HBM_PEAK_GBS}},
     }

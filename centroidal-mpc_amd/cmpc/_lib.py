@@ -73,7 +73,7 @@ EXPORTS = ['cmpc_create', 'cmpc_destroy', 'cmpc_last_error', 'cmpc_version', 'cm
            'cmpc_qp_solve', 'cmpc_accept', 'cmpc_scp_iterate', 'cmpc_solve_scp', 'cmpc_synchronize',
            'cmpc_get_linearization', 'cmpc_qp_sizes', 'cmpc_export_qp', 'cmpc_get_qp_solution',
            'cmpc_get_solution', 'cmpc_get_iteration_log', 'cmpc_get_timing', 'cmpc_timing_begin',
-           'cmpc_timing_end', 'cmpc_get_qp_iterations_total', 'cmpc_debug_stamps', 'cmpc_set_scp_mode',
+           'cmpc_timing_end', 'cmpc_get_qp_iterations_total', 'cmpc_debug_stamps', 'cmpc_get_qp_kernel', 'cmpc_set_scp_mode',
            'cmpc_get_linearization_point', 'cmpc_interpolate', 'cmpc_generate_contact_plans',
            'cmpc_upload_states', 'cmpc_get_contact_plans', 'cmpc_get_warm_start', 'cmpc_get_qp_info',
            'cmpc_comm_get_unique_id', 'cmpc_comm_init', 'cmpc_comm_destroy', 'cmpc_comm_bcast_params',
@@ -127,6 +127,7 @@ def load():
         'cmpc_timing_end': (i32, [h, P(Timing), P(ctypes.c_int)]),
         'cmpc_get_qp_iterations_total': (i32, [h, P(ctypes.c_int64)]),
         'cmpc_debug_stamps': (i32, [h, vp]),
+        'cmpc_get_qp_kernel': (i32, [h, ctypes.c_char_p, i32]),
         'cmpc_set_scp_mode': (i32, [h, i32]),
         'cmpc_get_linearization_point': (i32, [h, vp, vp, vp]),
         'cmpc_interpolate': (i32, [h, i32, vp, vp]),
@@ -509,6 +510,12 @@ class Solver:
         v = ctypes.c_int64(0)
         self._chk(self.lib.cmpc_get_qp_iterations_total(self.h, ctypes.byref(v)), 'cmpc_get_qp_iterations_total')
         return int(v.value)
+
+    def qp_kernel(self):
+        """Name of the QP kernel the library launches for the uploaded batch (cmpc_get_qp_kernel)."""
+        buf = ctypes.create_string_buffer(64)
+        self._chk(self.lib.cmpc_get_qp_kernel(self.h, buf, 64), 'cmpc_get_qp_kernel')
+        return buf.value.decode()
 
     def debug_stamps(self):
         out = np.zeros((self.B, 16), np.uint64)

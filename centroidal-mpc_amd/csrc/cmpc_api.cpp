@@ -1394,6 +1394,15 @@ int cmpc_get_qp_iterations_total(cmpc_handle h, int64_t *total) {
     });
 }
 
+int cmpc_get_qp_kernel(cmpc_handle h, char *buf, int n) {
+    return guard(h, [&] {
+        need(buf != nullptr && n > 0, "null output");
+        const int P = qp_group(h);
+        const std::string s = P ? "k_qp_group<" + std::to_string(P) + ">" : "k_qp_ipm<" + std::to_string(qp_waves(h)) + ">";
+        std::snprintf(buf, (size_t)n, "%s", s.c_str());
+    });
+}
+
 int cmpc_debug_stamps(cmpc_handle h, uint64_t *out) {
     return guard(h, [&] {
         need(out != nullptr, "null output");

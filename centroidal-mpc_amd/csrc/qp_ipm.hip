@@ -179,6 +179,7 @@ template <typename T, int ROBOT> struct Ctx {
     // multi-wave workgroups: w_x of knot k (k >= 1) parked here by phase_w and added to Schur block
     // k after the phase's barrier (add_wx), since block k's other terms come from another wave
     LdsT<T> *wxs = nullptr;
+    LdsT<T> *bus = nullptr;   // four-wave split w phases: B w_u of knot k at block 1 + k (add_wx)
     T *Sh = nullptr, *Sx = nullptr;   // four-wave workgroups: fill factors, separator scratch (schur_pt.hpp)
     int sp[3] = {0, 0, 0};            // four-wave workgroups: separator blocks
     LdsT<T> *sbv = nullptr, *hy = nullptr;   // separator right-hand-side terms, fill products
@@ -651,7 +652,8 @@ template <typename T, int ROBOT> __device__ __forceinline__ void load_knot_sl(co
         for (int e = 0; e < 12; ++e) kl.G[c][e] = st[S::CON + S::CS * c + S::G + e];
 }
 
-template <typename T, int ROBOT>
+// PART as in resid_knot: 0 the (L, t) block (facx), 1 the contacts (facu), -1 both
+template <typename T, int ROBOT, int PART = -1>
 __device__ __forceinline__ void phase_factor(const Ctx<T, ROBOT> &C, int k, const KnotSL<T, ROBOT> &kl) {
     using R_ = Rows<ROBOT>;
     constexpr int NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
@@ -663,6 +665,7 @@ __device__ __forceinline__ void phase_factor(const Ctx<T, ROBOT> &C, int k, cons
     // (L, t) block in push-through form (no D * r product, no cancellation as rows pin L or t),
     // see tr_factor; stored: M_LL = [Phi^-1]_LL = W_L^-1 - Z'Z + cw^2 g g' / den with
     // Z = L^-1 Y, g = Z' z1 (phase_sblock).  L, z1, den are recomputed where they are used.
+    if (PART != 1) {
     const T wl[3] = {C.iWx(6), C.iWx(7), C.iWx(8)};
     T Lk[36], z1[8], iden, dsl;
     tr_factor(C, s, lm, Lk, z1, iden, dsl);
@@ -686,9 +689,10 @@ __device__ __forceinline__ void phase_factor(const Ctx<T, ROBOT> &C, int k, cons
             for (int j = 0; j < 8; ++j) zz += Z[j][i] * Z[j][q];
             fx[FX_ML + p] = (i == q ? wl[i] : T(0)) - zz + C.cw * C.cw * g[i] * g[q] * iden;
         }
+    }
     if (k >= N) return;
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
+    for (int c = 0; c < (PART != 0 ? NC : 0); ++c) {
         const SV<T> fu = C.kv(WF(facu), k) + c * FU;
         const bool act = (msk >> c) & 1u;
         // Winvd: inverse diagonal of W' (CoP rows fold into their coordinate's diagonal)
@@ -1428,24 +1432,27 @@ __device__ void tw_solve_back(const T *Xs, int NB, int m, LdsT<T> *vb, LdsT<T> *
 // r_hat = r_i - r_c / lambda for the rows of knot k.  corr 0 (predictor): r_c = s lambda; 1
 // (corrector): r_c = s lambda + ds_aff dlambda_aff - sigma mu; 2 (refinement): r_c = the dsa
 // field, which then holds the complementarity residual of the corrector direction (phase_lres)
-template <typename T, int ROBOT>
+// rows [R0, R1): all of them, or one part's (PART as in resid_knot)
+template <typename T, int ROBOT, int R0 = 0, int R1 = Rows<ROBOT>::NI>
 __device__ __forceinline__ void rhat_rows(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu, const T *s, const T *lm,
                                           T *rh) {
     constexpr int NI = Rows<ROBOT>::NI;
     const unsigned msk = C.cmask(k);
     // every row's loads in one batch (a branch per row serialized them)
     T rd[NI], cc[NI];
-    ldv(C.kv(WF(rdi), k), rd);
+    const SV<T> rdi = C.kv(WF(rdi), k);
 #pragma unroll
-    for (int r = 0; r < NI; ++r) cc[r] = T(0);
+    for (int r = R0; r < R1; ++r) { rd[r] = rdi[r]; cc[r] = T(0); }
     if (corr) {   // corrector: + ds_aff dlambda_aff - sigma mu (the product, stored by the predictor)
         T a[NI];
-        ldv(C.kv(WF(dsa), k), a);
+        const SV<T> dsa = C.kv(WF(dsa), k);
 #pragma unroll
-        for (int r = 0; r < NI; ++r) cc[r] = corr == 2 ? a[r] : a[r] - sigma_mu;
+        for (int r = R0; r < R1; ++r) a[r] = dsa[r];
+#pragma unroll
+        for (int r = R0; r < R1; ++r) cc[r] = corr == 2 ? a[r] : a[r] - sigma_mu;
     }
 #pragma unroll
-    for (int r = 0; r < NI; ++r) {
+    for (int r = R0; r < R1; ++r) {
         const bool pr = Ctx<T, ROBOT>::present_m(msk, r);
         const T sr = s[r], lr = lm[r];
         const T rc = (corr == 2 ? T(0) : sr * lr) + cc[r];
@@ -1457,22 +1464,26 @@ __device__ __forceinline__ void rhat_rows(const Ctx<T, ROBOT> &C, int k, int cor
 // (5a) particular solution w = Phi^-1 (r_d + G' D rhat) (friction rows in push-through form)
 // getG(c, G): the friction rows of contact c (from registers in the predictor, which shares the
 // factor phase's loads, or from the stage record)
-template <typename T, int ROBOT, typename GF>
+// PART as in resid_knot: 0 the (x, t) part (w_x, the trust-region / slack rows of r_hat, the
+// right-hand side but B w_u), 1 the controls (w_u, the contact rows of r_hat, B w_u into the side
+// array C.bus, subtracted with add_wx), -1 both
+template <typename T, int ROBOT, typename GF, int PART = -1>
 __device__ __forceinline__ void phase_w_core(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu,
                                              const T (&sv)[Rows<ROBOT>::NI], const T (&lv)[Rows<ROBOT>::NI], GF &&getG) {
     using R_ = Rows<ROBOT>;
     constexpr int NI = R_::NI, NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
     const int N = C.N;
     const bool hu = k < N;
+    constexpr int RA = PART == 1 ? R_::FR : 0, RB = PART == 0 ? R_::FR : NI;   // this part's rows
     T rh[NI];
-    rhat_rows(C, k, corr, sigma_mu, sv, lv, rh);   // kept for phase_dz (stored below)
+    rhat_rows<T, ROBOT, RA, RB>(C, k, corr, sigma_mu, sv, lv, rh);   // kept for phase_dz (stored below)
     T rdx[9], rdu[NU];
     ldv(C.kv(WF(rdx), k), rdx);
     ldv(C.kv(WF(rdu), k), rdu);   // k = N: unused
     const T rdt = C.kv(WF(rdt), k)[0];
     T wx[9], wt;
     for (int i = 0; i < 6; ++i) wx[i] = C.iWx(i) * rdx[i];
-    {   // (L, t): w = -(local solve with v = -r_d)
+    if (PART != 1) {   // (L, t): w = -(local solve with v = -r_d)
         T Lk[36], z1[8], iden, dsl;
         tr_factor(C, sv, lv, Lk, z1, iden, dsl);
         const T vL[3] = {-rdx[6], -rdx[7], -rdx[8]};
@@ -1482,7 +1493,7 @@ __device__ __forceinline__ void phase_w_core(const Ctx<T, ROBOT> &C, int k, int 
         wt = -dt;
     }
     T ou[NU];
-    if (hu) {
+    if (hu && PART != 0) {
         T vu[NU];
         for (int i = 0; i < NU; ++i) vu[i] = rdu[i];
         if (ROBOT == 1) {   // CoP rows (D-form, folded into W_cop); absent rows: lambda = 0 -> D = 0, rhat = 0
@@ -1522,8 +1533,12 @@ __device__ __forceinline__ void phase_w_core(const Ctx<T, ROBOT> &C, int k, int 
     }
     // stores
     (void)wt;   // w_x, w_t enter only the right-hand side below; w_u is read by phase_dz
-    if (hu) stv(C.kv(WF(wu), k), ou);
-    stv(C.kv(WF(rh), k), rh);
+    if (hu && PART != 0) stv(C.kv(WF(wu), k), ou);
+    {
+        const SV<T> rhs = C.kv(WF(rh), k);
+#pragma unroll
+        for (int r = RA; r < RB; ++r) rhs[r] = rh[r];
+    }
     // the Schur right-hand side, fused: block 1 + k = r_k - A_k wx_k - B_k wu_k + wx_{k+1}.  Thread
     // k writes all but the last term; after a wave-level fence (block k was written by lane k - 1
     // in this pass or an earlier one: the lanes of the one wave run in lockstep) it adds its own
@@ -1531,6 +1546,14 @@ __device__ __forceinline__ void phase_w_core(const Ctx<T, ROBOT> &C, int k, int 
     {
         using S = Stage<ROBOT>;
         LdsT<T> *vb = C.vb;
+        if (PART == 1) {   // B w_u of knot k into the side array (block 1 + k)
+            if (hu) {
+                T bu[9];
+                opB<T, ROBOT>(C.st(k), ou, bu);
+                for (int i = 0; i < 9; ++i) C.bus[(1 + k) * 9 + i] = bu[i];
+            }
+            return;
+        }
         T r0[9], r1[9];
         ldv(C.bv(WF(rde), k == N ? N + 1 : 0), r0);   // boundary rows (k = 0: init, k = N: final)
         ldv(C.bv(WF(rde), hu ? 1 + k : 0), r1);       // dynamics rows of knot k
@@ -1540,8 +1563,8 @@ __device__ __forceinline__ void phase_w_core(const Ctx<T, ROBOT> &C, int k, int 
             T ax[9], bu[9];
             const auto st = C.st(k);
             opA(st + S::W, C.beta, wx, ax);
-            opB<T, ROBOT>(st, ou, bu);
-            for (int i = 0; i < 9; ++i) vb[(1 + k) * 9 + i] = r1[i] - (ax[i] + bu[i]);
+            if (PART != 0) opB<T, ROBOT>(st, ou, bu);
+            for (int i = 0; i < 9; ++i) vb[(1 + k) * 9 + i] = r1[i] - (ax[i] + (PART != 0 ? bu[i] : T(0)));
         }
         if (C.wxs) {
             if (k >= 1)
@@ -1554,23 +1577,31 @@ __device__ __forceinline__ void phase_w_core(const Ctx<T, ROBOT> &C, int k, int 
     }
 }
 // the deferred last term of the fused right-hand side (multi-wave workgroups): block k += w_x,k
-template <typename T, int NTT> __device__ __forceinline__ void add_wx(LdsT<T> *vb, const LdsT<T> *wxs, int N) {
-    for (int e = 9 + (int)(threadIdx.x & (NTT - 1)); e < (N + 1) * 9; e += NTT) vb[e] += wxs[e];
+// (and, after split w phases, minus the control part's B w_u, block 1 + k of bus)
+template <typename T, int NTT>
+__device__ __forceinline__ void add_wx(LdsT<T> *vb, const LdsT<T> *wxs, int N, const LdsT<T> *bus = nullptr) {
+    if (bus)
+        for (int e = 9 + (int)(threadIdx.x & (NTT - 1)); e < (N + 1) * 9; e += NTT) vb[e] += wxs[e] - bus[e];
+    else
+        for (int e = 9 + (int)(threadIdx.x & (NTT - 1)); e < (N + 1) * 9; e += NTT) vb[e] += wxs[e];
 }
-template <typename T, int ROBOT> __device__ __forceinline__ void phase_w(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu) {
+template <typename T, int ROBOT, int PART = -1> __device__ __forceinline__ void phase_w(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu) {
     using S = Stage<ROBOT>;
     constexpr int NI = Rows<ROBOT>::NI;
     T sv[NI], lv[NI];
     ldv(C.kv(WF(s), k), sv);
     ldv(C.kv(WF(l), k), lv);
     const auto st = C.st(k);
-    phase_w_core(C, k, corr, sigma_mu, sv, lv, [&](int c, T (&G)[12]) { ldv(st + (S::CON + S::CS * c + S::G), G); });
+    auto getG = [&](int c, T (&G)[12]) { ldv(st + (S::CON + S::CS * c + S::G), G); };
+    phase_w_core<T, ROBOT, decltype(getG) &, PART>(C, k, corr, sigma_mu, sv, lv, getG);
 }
-template <typename T, int ROBOT> __device__ __forceinline__ void phase_w_pred(const Ctx<T, ROBOT> &C, int k, const KnotSL<T, ROBOT> &kl) {
-    phase_w_core(C, k, 0, T(0), kl.s, kl.l, [&](int c, T (&G)[12]) {
+template <typename T, int ROBOT, int PART = -1>
+__device__ __forceinline__ void phase_w_pred(const Ctx<T, ROBOT> &C, int k, const KnotSL<T, ROBOT> &kl) {
+    auto getG = [&](int c, T (&G)[12]) {
 #pragma unroll
         for (int e = 0; e < 12; ++e) G[e] = kl.G[c][e];
-    });
+    };
+    phase_w_core<T, ROBOT, decltype(getG) &, PART>(C, k, 0, T(0), kl.s, kl.l, getG);
 }
 
 
@@ -2216,16 +2247,34 @@ __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT>
         if (leave()) break;
         // ---- Phi factors and the predictor's particular solution (knot-local), then the S blocks
         // and the predictor's Schur right-hand side
-        for (int k = tid; k < K1; k += G) {
-            KnotSL<T, ROBOT> kl;
-            load_knot_sl(C, k, kl);
-            phase_factor<T, ROBOT>(C, k, kl);
-            phase_w_pred<T, ROBOT>(C, k, kl);
+        if constexpr (split_knots<G>()) {
+            if (__builtin_amdgcn_readfirstlane(tid) < 128) {
+                for (int k = tid & 127; k < K1; k += 128) {
+                    KnotSL<T, ROBOT> kl;
+                    load_knot_sl(C, k, kl);
+                    phase_factor<T, ROBOT, 0>(C, k, kl);
+                    phase_w_pred<T, ROBOT, 0>(C, k, kl);
+                }
+            } else {
+                for (int k = tid & 127; k < K1; k += 128) {
+                    KnotSL<T, ROBOT> kl;
+                    load_knot_sl(C, k, kl);
+                    phase_factor<T, ROBOT, 1>(C, k, kl);
+                    phase_w_pred<T, ROBOT, 1>(C, k, kl);
+                }
+            }
+        } else {
+            for (int k = tid; k < K1; k += G) {
+                KnotSL<T, ROBOT> kl;
+                load_knot_sl(C, k, kl);
+                phase_factor<T, ROBOT>(C, k, kl);
+                phase_w_pred<T, ROBOT>(C, k, kl);
+            }
         }
         gsync<G, WG>();
         STAMP(1);
         if (leave()) break;
-        if (G > 64) add_wx<T, G>(C.vb, C.wxs, N);
+        if (G > 64) add_wx<T, G>(C.vb, C.wxs, N, C.bus);
         for (int k = tid; k < K1; k += G) phase_sblock<T, ROBOT>(C, k);
         gsync<G, WG>();
         STAMP(2);
@@ -2270,10 +2319,18 @@ __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT>
         T alpha = T(1);
         for (int corr = 0; corr < 2; ++corr) {
             if (corr) {
-                for (int k = tid; k < K1; k += G) phase_w<T, ROBOT>(C, k, corr, sigma_mu);
+                if constexpr (split_knots<G>()) {
+                    if (__builtin_amdgcn_readfirstlane(tid) < 128) {
+                        for (int k = tid & 127; k < K1; k += 128) phase_w<T, ROBOT, 0>(C, k, corr, sigma_mu);
+                    } else {
+                        for (int k = tid & 127; k < K1; k += 128) phase_w<T, ROBOT, 1>(C, k, corr, sigma_mu);
+                    }
+                } else {
+                    for (int k = tid; k < K1; k += G) phase_w<T, ROBOT>(C, k, corr, sigma_mu);
+                }
                 gsync<G, WG>();
                 if (G > 64) {
-                    add_wx<T, G>(C.vb, C.wxs, N);
+                    add_wx<T, G>(C.vb, C.wxs, N, C.bus);
                     gsync<G, WG>();
                 }
                 STAMP(4);
@@ -2401,6 +2458,7 @@ __global__ void __launch_bounds__(NTT, NTT == 128 ? QP_MIN_WAVES_2W : QP_MIN_WAV
         pt_seps<T>(NB, C.sp);
         C.sbv = (LdsT<T> *)sbv_s;
         C.hy = C.wxs + vec;
+        C.bus = C.hy + vec;
     }
     IpmState<T> S = ipm_state0<T>();
     ipm_start<T, ROBOT, NTT, NTT>(d, C, b);
@@ -2522,6 +2580,7 @@ __global__ void __launch_bounds__(64 * P, 1) k_qp_group(DevBuf<T> d, const int *
             pt_seps<T>(NB, C.sp);
             C.sbv = (LdsT<T> *)sbv_s;
             C.hy = region((r + 2) % P);
+            C.bus = region((r + 3) % P);
             L.ring = Rw + vec;
             L.shl = Rw + vec + GL::RING;
         } else {   // the two ends' sweeps run on the halves of wave 0; the ends' scratch is R's
@@ -2647,9 +2706,10 @@ int ipm_pair_max_batch() { return ORD_MAXB; }
 size_t ipm_lds_bytes(int N, int prec_bytes, int nt) {
     const size_t vec = (((size_t)(N + 2) * 9 + 7) & ~size_t(7));
     // vb, the sweep rings (two; one per wave with four waves), the w_x side array, the fill
-    // products of the four-wave solves; at least one covariance scan's buffers (the scan jobs)
+    // products of the four-wave solves and their split w phases' B w_u side array; at least one
+    // covariance scan's buffers (the scan jobs)
     const size_t nring = nt >= 256 ? 4 : 2;
-    return std::max<size_t>(vec + nring * SWEEP_LDS + (nt > 64 ? vec : 0) + (nt >= 256 ? vec : 0), SCAN_LDS) * prec_bytes;
+    return std::max<size_t>(vec + nring * SWEEP_LDS + (nt > 64 ? vec : 0) + (nt >= 256 ? 2 * vec : 0), SCAN_LDS) * prec_bytes;
 }
 
 size_t ipm_workspace_elems(int N, int robot) {

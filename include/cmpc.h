@@ -284,6 +284,10 @@ int cmpc_get_qp_iterations_total(cmpc_handle h, int64_t *total);
 /* Diagnostic builds (libcmpc_diag.so, -DCMPC_STAMPS): per-problem shader-cycle counters of the
  * QP kernel's phases, (B, 16); zeros in the production library. */
 int cmpc_debug_stamps(cmpc_handle h, uint64_t *out);
+/* The QP kernel the next cmpc_qp_solve / cmpc_scp_iterate launches for the uploaded batch, e.g.
+ * "k_qp_group<4>" (four problems per four-wave workgroup) or "k_qp_ipm<2>" (one problem per
+ * two-wave workgroup); written NUL-terminated into buf (at most n bytes).  For measurement labels. */
+int cmpc_get_qp_kernel(cmpc_handle h, char *buf, int n);
 
 /* ---- multi-GPU batch split over RCCL (one process per GPU, one handle per process) ----
  * The problems are independent: nothing crosses GPUs inside the SCP loop.  Rank r owns a

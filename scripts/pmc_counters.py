@@ -16,7 +16,7 @@ import json
 import os
 import sys
 
-KERNELS = ('k_qp_ipm', 'k_linearize', 'k_accept', 'k_assemble')
+KERNELS = ('k_qp_group', 'k_qp_ipm', 'k_linearize', 'k_accept', 'k_assemble')
 F64_MATRIX_PEAK_TFLOPS = 78.6
 
 

@@ -29,7 +29,7 @@ def main():
     out = sys.argv[3] if len(sys.argv) > 3 else os.path.join(os.path.dirname(__file__), '..', 'profiles',
                                                               'qp_pmc_traffic.json')
     fe, wr = per_kernel(fdir, 'FETCH_SIZE'), per_kernel(wdir, 'WRITE_SIZE')
-    qp = [k for k in fe if 'k_qp_ipm' in k][0]
+    qp = sorted(k for k in fe if 'k_qp_ipm' in k or 'k_qp_group' in k)[0]   # the batch's QP kernel
     fkb, fn = fe[qp]
     wkb, wn = wr[qp]
     per_launch = (2.0 * fkb / fn + wkb / wn) * 1024.0

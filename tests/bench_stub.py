@@ -70,6 +70,9 @@ class StubSolver:
     def qp_solution(self, with_y=True):
         return np.zeros((self.B, 1)), None, np.ones(self.B, np.int32), np.full(self.B, 5, np.int32)
 
+    def qp_kernel(self):
+        return 'stub'
+
     def qp_info(self):
         return np.full(self.B, 0.5), np.zeros(self.B, np.int32)
 
