@@ -2177,12 +2177,25 @@ __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT>
 #endif
     int status = S.status, it = S.it, stall = S.stall, n_refine = S.n_refine;
     T mu_prev = S.mu_prev, merit = S.merit, prim_prev = S.prim_prev;
+    // k_qp_group: have the other problems of the workgroup finished?  A group of two waves decides
+    // once for both (its first thread reads the count and publishes it behind the group barrier),
+    // so its waves never part ways
+    auto want_yield = [&]() -> bool {
+        if (!yield) return false;
+        if constexpr (G > 64 && G < WG) {
+            if (tid == 0) L.red[31] = T(__builtin_amdgcn_readfirstlane(*yield) >= yield_at ? 1 : 0);
+            gsync<G, WG>();
+            return L.red[31] != T(0);
+        } else {
+            return __builtin_amdgcn_readfirstlane(*yield) >= yield_at;
+        }
+    };
     // it == 0 is the initialization step: one full Newton step from s = lambda = 1 gives an
     // equality-feasible least-squares start; s and lambda are then floored row by row (Solo12)
     // or shifted by 1 + the largest violation (TALOS), see init_s_knot.
     for (it = S.it; it <= max_iter; ++it) {
         // k_qp_group: the other waves have finished, so this problem continues on all of them
-        if (yield && __builtin_amdgcn_readfirstlane(*yield) >= yield_at) { S.yielded = 1; break; }
+        if (want_yield()) { S.yielded = 1; break; }
         const bool init = (it == 0);
         const int stall0 = stall;
         const T mu_prev0 = mu_prev, prim_prev0 = prim_prev;
@@ -2237,7 +2250,7 @@ __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT>
         // 0.57 of the one-wave time per Newton step, redoing beats finishing the iteration alone
         // while less than ~40% of it is done (residual 19%, Phi factors and w 10%, S blocks 4%).
         auto leave = [&]() {
-            if (!(yield && __builtin_amdgcn_readfirstlane(*yield) >= yield_at)) return false;
+            if (!want_yield()) return false;
             S.yielded = 1;
             stall = stall0;
             mu_prev = mu_prev0;
@@ -2501,64 +2514,75 @@ __global__ void __launch_bounds__(NTT, NTT == 128 ? QP_MIN_WAVES_2W : QP_MIN_WAV
 // all waves finish the last problem, it keeps its region; the other regions hold the w_x side
 // array and (P = 4) the fill products in their Schur-vector slots, and each wave uses its own
 // region's first ring and recurrence scratch.
-template <typename T> struct GroupLds {
-    static constexpr int RING = 2 * SWEEP_LDS, SH = 2 * TW_SCRATCH, RED = 32, WTS = 48;
+template <typename T, int W = 1> struct GroupLds {
+    // W = 2: the problem's w_x side array after its Schur vector; recurrence scratch for two
+    // four-chain waves (the last problem's four waves use both regions' scratch and rings)
+    static constexpr int RING = 2 * SWEEP_LDS, SH = W == 1 ? 2 * TW_SCRATCH : 2 * PT_SCRATCH, RED = 32, WTS = 48;
     static constexpr int CMS = (KPC + 8 * (int)sizeof(T) - 1) / (8 * (int)sizeof(T)) * 8;
-    static_assert(SH >= PT_SCRATCH, "a region holds one wave's four-chain scratch");
+    static_assert(SH >= PT_SCRATCH * W && SH >= 2 * TW_SCRATCH, "a region holds its waves' recurrence scratch");
+    static_assert(W == 1 || SCAN_LDS <= 2 * SWEEP_LDS, "a wave's half of a region holds a covariance scan");
     __host__ __device__ static constexpr int vec(int N) { return ((N + 2) * 9 + 7) & ~7; }
-    __host__ __device__ static constexpr int region(int N) { return vec(N) + RING + SH + RED + WTS + CMS; }
+    __host__ __device__ static constexpr int region(int N) { return W * vec(N) + RING + SH + RED + WTS + CMS; }
 };
 
-template <typename T, int ROBOT, int P>
-__global__ void __launch_bounds__(64 * P, 1) k_qp_group(DevBuf<T> d, const int *order, int only_active, int share,
-                                                        int max_iter, T eps_abs, T eps_rel, T eta, T floor_s,
-                                                        T floor_l) {
+// P problems of W waves each per workgroup (WG = 64 P W threads): P = 2 or 4 with W = 1, or P = 2
+// with W = 2 (the 512-problem shards: two two-wave problems, the last one on all four waves; its
+// waves synchronize through the LDS barrier of gsync<128, 256>).
+template <typename T, int ROBOT, int P, int W>
+__global__ void __launch_bounds__(64 * P * W, 1) k_qp_group(DevBuf<T> d, const int *order, int only_active, int share,
+                                                            int max_iter, T eps_abs, T eps_rel, T eta, T floor_s,
+                                                            T floor_l) {
     extern __shared__ __attribute__((aligned(16))) unsigned char dsmem[];
-    using GL = GroupLds<T>;
-    constexpr int WG = 64 * P;
+    using GL = GroupLds<T, W>;
+    constexpr int G = 64 * W, WG = G * P;
+    static_assert(WG == 128 || WG == 256, "two or four waves per workgroup");
     __shared__ int nfree, rem;
     __shared__ IpmState<T> Ss;
-    __shared__ T sbv_s[P >= 4 ? 6 * 9 : 1];
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, N = d.N, NB = N + 2;
+    __shared__ T sbv_s[WG >= 256 ? 6 * 9 : 1];
+    const int w = threadIdx.x / G, lane = threadIdx.x & 63, N = d.N, NB = N + 2;
     const int RG = GL::region(N), vec = GL::vec(N);
     LdsT<T> *base = (LdsT<T> *)reinterpret_cast<T *>(dsmem);
     auto region = [&](int v) { return base + (size_t)v * RG; };
-    auto wts_of = [&](LdsT<T> *R) { return R + vec + GL::RING + GL::SH + GL::RED; };
-    auto cms_of = [&](LdsT<T> *R) { return (LdsT<uint8_t> *)(R + vec + GL::RING + GL::SH + GL::RED + GL::WTS); };
+    auto after_vec = [&](LdsT<T> *R) { return R + W * vec; };
+    auto wts_of = [&](LdsT<T> *R) { return after_vec(R) + GL::RING + GL::SH + GL::RED; };
+    auto cms_of = [&](LdsT<T> *R) { return (LdsT<uint8_t> *)(after_vec(R) + GL::RING + GL::SH + GL::RED + GL::WTS); };
     if (threadIdx.x == 0) {
         nfree = 0;
         rem = -1;
+        if (W == 2) for (int i = 0; i < 4; ++i) cmpc_hbar[i] = 0;
     }
     __syncthreads();
-    // one problem per wave.  The problem index is the same on every lane of the wave: as a uniform
-    // (scalar) value, every pointer derived from it stays in SGPRs (as a per-lane value the one-wave
-    // mode spilled 888 B per lane and ran 11% slower than k_qp_ipm<.., 64>)
+    // one problem per group of W waves.  The problem index is the same on every lane of the wave:
+    // as a uniform (scalar) value, every pointer derived from it stays in SGPRs (as a per-lane value
+    // the one-wave mode spilled 888 B per lane and ran 11% slower than k_qp_ipm<.., 64>)
     const int slot = P * blockIdx.x + w;
     const int b = __builtin_amdgcn_readfirstlane(slot < d.B ? order[slot] : -1);
+    const int gt = threadIdx.x & (G - 1);   // thread of the group
     if (b >= 0 && (!only_active || d.scp[b].active)) {
         LdsT<T> *R = region(w);
         Ctx<T, ROBOT> C{};
-        ctx_setup<T, ROBOT, 64>(d, b, C, wts_of(R), cms_of(R), floor_s, floor_l);
-        gsync<64, WG>();
+        ctx_setup<T, ROBOT, G>(d, b, C, wts_of(R), cms_of(R), floor_s, floor_l);
+        gsync<G, WG>();
         C.vb = R;
+        if (W == 2) C.wxs = R + vec;
         IpmLds<T> L;
-        L.ring = R + vec + (lane >> 5) * SWEEP_LDS;
-        L.shl = R + vec + GL::RING;
-        L.red = (T *)(R + vec + GL::RING + GL::SH);
+        L.ring = after_vec(R) + (lane >> 5) * SWEEP_LDS;   // the two ends' sweeps: halves of the group's first wave
+        L.shl = after_vec(R) + GL::RING;
+        L.red = (T *)(after_vec(R) + GL::RING + GL::SH);
         IpmState<T> S = ipm_state0<T>();
-        ipm_start<T, ROBOT, 64, WG>(d, C, b);
-        ipm_loop<T, ROBOT, 64, WG>(d, C, b, S, L, max_iter, eps_abs, eps_rel, eta,
-                                   share ? (const volatile LdsT<int> *)&nfree : nullptr, P - 1);
+        ipm_start<T, ROBOT, G, WG>(d, C, b);
+        ipm_loop<T, ROBOT, G, WG>(d, C, b, S, L, max_iter, eps_abs, eps_rel, eta,
+                                  share ? (const volatile LdsT<int> *)&nfree : nullptr, P - 1);
         if (S.yielded) {
-            if (lane == 0) {
+            if (gt == 0) {
                 Ss = S;
                 rem = w;
             }
         } else {
-            if (lane == 0) atomicAdd(&nfree, 1);   // free: the last problem may leave its loop while
-            ipm_finish<T, ROBOT, 64>(d, C, b, S);  // this wave writes the outputs (global memory only)
+            if (gt == 0) atomicAdd(&nfree, 1);   // free: the last problem may leave its loop while
+            ipm_finish<T, ROBOT, G>(d, C, b, S); // this group writes the outputs (global memory only)
         }
-    } else if (lane == 0) {
+    } else if (gt == 0) {
         atomicAdd(&nfree, 1);
     }
     __syncthreads();   // the first s_barrier of any wave since the start
@@ -2571,23 +2595,33 @@ __global__ void __launch_bounds__(64 * P, 1) k_qp_group(DevBuf<T> d, const int *
         ctx_setup<T, ROBOT, WG>(d, b2, C, wts_of(R), cms_of(R), floor_s, floor_l);   // (the same values)
         __syncthreads();
         C.vb = R;
-        C.wxs = region((r + 1) % P);
-        LdsT<T> *Rw = region(w);   // this wave's region: its first ring and recurrence scratch
         IpmLds<T> L;
-        if constexpr (P >= 4) {
+        const int wv = threadIdx.x >> 6;
+        if constexpr (WG >= 256) {   // four waves: four chains, split knots
             C.Sh = C.ws + Ws<ROBOT>::Sh;
             C.Sx = C.ws + Ws<ROBOT>::Sx;
             pt_seps<T>(NB, C.sp);
             C.sbv = (LdsT<T> *)sbv_s;
-            C.hy = region((r + 2) % P);
-            C.bus = region((r + 3) % P);
-            L.ring = Rw + vec;
-            L.shl = Rw + vec + GL::RING;
-        } else {   // the two ends' sweeps run on the halves of wave 0; the ends' scratch is R's
-            L.ring = R + vec + (lane >> 5) * SWEEP_LDS;
-            L.shl = R + vec + GL::RING;
+            if (W == 1) {   // the other regions' Schur-vector slots; each wave its own region's ring, scratch
+                C.wxs = region((r + 1) % P);
+                C.hy = region((r + 2) % P);
+                C.bus = region((r + 3) % P);
+                L.ring = after_vec(region(wv));
+                L.shl = after_vec(region(wv)) + GL::RING;
+            } else {        // R's w_x slot; the other region's two vector slots; wave v: ring and
+                            // scratch v % 2 of region v / 2
+                C.wxs = R + vec;
+                C.hy = region(1 - r);
+                C.bus = region(1 - r) + vec;
+                L.ring = after_vec(region(wv >> 1)) + (wv & 1) * SWEEP_LDS;
+                L.shl = after_vec(region(wv >> 1)) + GL::RING + (wv & 1) * PT_SCRATCH;
+            }
+        } else {   // two waves, pairs of one-wave problems: the ends' sweeps on the halves of wave 0
+            C.wxs = region(1 - r);
+            L.ring = after_vec(R) + (lane >> 5) * SWEEP_LDS;
+            L.shl = after_vec(R) + GL::RING;
         }
-        L.red = (T *)(R + vec + GL::RING + GL::SH);
+        L.red = (T *)(after_vec(R) + GL::RING + GL::SH);
         IpmState<T> S = Ss;
         S.yielded = 0;
 #ifdef CMPC_STAMPS
@@ -2606,7 +2640,7 @@ __global__ void __launch_bounds__(64 * P, 1) k_qp_group(DevBuf<T> d, const int *
     // covariance scan jobs of a deterministic batch, each wave on its own (as in k_qp_ipm<.., 64>)
     if (d.scan_ctr) {
         __syncthreads();   // the dynamic LDS is free from here on
-        LdsT<T> *R = region(w);
+        LdsT<T> *R = base + (size_t)(threadIdx.x >> 6) * (RG / W / 8 * 8);   // a slice per wave
         for (;;) {
             int j = 0;
             if (lane == 0) j = (int)atomicAdd(d.scan_ctr, 1u);
@@ -2686,8 +2720,9 @@ template <typename T> __global__ void __launch_bounds__(1024) k_qp_order(DevBuf<
     template __global__ void k_qp_ipm<T, R, 64>(DevBuf<T>, int, int, T, T, T, T, T);     \
     template __global__ void k_qp_ipm<T, R, 128>(DevBuf<T>, int, int, T, T, T, T, T);    \
     template __global__ void k_qp_ipm<T, R, 256>(DevBuf<T>, int, int, T, T, T, T, T);    \
-    template __global__ void k_qp_group<T, R, 2>(DevBuf<T>, const int *, int, int, int, T, T, T, T, T); \
-    template __global__ void k_qp_group<T, R, 4>(DevBuf<T>, const int *, int, int, int, T, T, T, T, T);
+    template __global__ void k_qp_group<T, R, 2, 1>(DevBuf<T>, const int *, int, int, int, T, T, T, T, T); \
+    template __global__ void k_qp_group<T, R, 4, 1>(DevBuf<T>, const int *, int, int, int, T, T, T, T, T); \
+    template __global__ void k_qp_group<T, R, 2, 2>(DevBuf<T>, const int *, int, int, int, T, T, T, T, T);
 INST(double, 0)
 INST(double, 1)
 INST(float, 0)
@@ -2696,9 +2731,10 @@ INST(float, 1)
 template __global__ void k_qp_order<double>(DevBuf<double>, int, int, int *);
 template __global__ void k_qp_order<float>(DevBuf<float>, int, int, int *);
 
-// dynamic LDS of k_qp_group with P problems per workgroup
-size_t ipm_group_lds_bytes(int N, int prec_bytes, int P) {
-    const size_t e = prec_bytes == 8 ? GroupLds<double>::region(N) : GroupLds<float>::region(N);
+// dynamic LDS of k_qp_group with P problems of W waves per workgroup
+size_t ipm_group_lds_bytes(int N, int prec_bytes, int P, int W) {
+    const size_t e = W == 1 ? (prec_bytes == 8 ? GroupLds<double, 1>::region(N) : GroupLds<float, 1>::region(N))
+                            : (prec_bytes == 8 ? GroupLds<double, 2>::region(N) : GroupLds<float, 2>::region(N));
     return (size_t)P * e * prec_bytes;
 }
 int ipm_pair_max_batch() { return ORD_MAXB; }

@@ -1,15 +1,21 @@
 #!/bin/bash
-# Round-end evidence at HEAD: cycle stamps, rocprof + PMC passes and the default bench line
-# (scripts/gpu_profile.sh), the other BASELINE configs (scripts/gpu_configs.sh) and one GPU's step
-# at the strong-scaling shard sizes (512 / 256 / 128 problems of the metric config).
+# Round-end check at HEAD: smoke, GPU suite, default bench line; then the two-wave group A/B
+# (on / unshared / off, CMPC_QP_GROUP2W=1) on the 512-problem shard.
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-TAG=${1:-r02c}
-timeout -k 10 200 python scripts/stamps.py trot 100 1024 > gpurun_out/stamps_$TAG.log 2>&1 || { tail -20 gpurun_out/stamps_$TAG.log; exit 1; }
-bash scripts/gpu_profile.sh $TAG || exit 1
-bash scripts/gpu_configs.sh > gpurun_out/configs_$TAG.jsonl || exit 1
-for nb in 512 256 128; do
-  timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-extras --batch $nb > gpurun_out/shard_$nb.json 2> gpurun_out/shard_$nb.err || { tail -20 gpurun_out/shard_$nb.err; exit 1; }
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { cat gpurun_out/smoke.log; exit 1; }
+tail -1 gpurun_out/smoke.log
+timeout -k 10 700 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread -rf > gpurun_out/pytest_gpu_final.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_final.log; exit 1; }
+tail -1 gpurun_out/pytest_gpu_final.log
+timeout -k 10 600 python3 bench.py > gpurun_out/bench_final.json 2> gpurun_out/bench_final.err || { tail -20 gpurun_out/bench_final.err; exit 1; }
+python3 -c "
+import json; d=json.loads(open('gpurun_out/bench_final.json').read().strip().splitlines()[-1]); print('bench', round(d['value']), d['roofline']['kernel'], 'frac %.3f' % d['roofline']['frac'], 'early', round(d['early_exit']['value']))"
+B="python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-extras --batch 512"
+for i in 1 2; do
+  CMPC_QP_GROUP2W=1 timeout -k 10 200 $B > gpurun_out/g2_on_$i.json 2>&1 || exit 1
+  CMPC_QP_GROUP2W=1 CMPC_QP_PAIR=2 timeout -k 10 200 $B > gpurun_out/g2_noshare_$i.json 2>&1 || exit 1
+  timeout -k 10 200 $B > gpurun_out/g2_off_$i.json 2>&1 || exit 1
 done
-cat gpurun_out/shard_*.json
+for f in gpurun_out/g2_*.json; do python3 -c "
+import json; d=json.loads(open('$f').read().strip().splitlines()[-1]); print('$f', round(d['value']), 'qp_ms %.4f' % d['phase_ms_per_step']['qp_ms'], d['roofline']['kernel'])"; done
