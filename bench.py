@@ -21,15 +21,19 @@ Extra fields ("Measurement"):
                 priced with the robot's own per-knot sizes, x IPM iterations actually run) / its
                 mean duration from HIP events recorded on the library's stream over the timed
                 region; ``compulsory`` prices the kernel's own minimum traffic per Newton step.
-  early_exit    the reference's semantics (src/scp_solver.py:133-134): solve until every problem
-                has left the loop, then copy X, U, K, Sigma to the host; SCP iterations executed /
-                wall time.
+  early_exit    the reference's semantics (src/scp_solver.py:118-179, a fresh solve per call): a
+                never-solved batch of the same shape (other seeds), solved until every problem has
+                left the loop, then X, U, K, Sigma copied to the host; SCP iterations executed / wall
+                time.  Its first QP launch has no Newton counts to group problems by.
+  repeats       the timed region run 5 more times (median of 5); ``value`` is the first
+                region, as the bench contract asks.
   qp_exit       QP exit-status histogram and refinement counts of the last timed step.
   cpu_baseline  the oracle (numpy/scipy restatement of the reference path, OSQP algorithm at the
                 reference's eps 1e-7 with polish) on bounded samples, rank 0 at N = 1 only:
                 throughput over the box's CPU share, single-core latency and early exit.
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -73,6 +77,32 @@ def compulsory_qp_bytes(N, ipm_iters_total, w, robot='solo12'):
     sblocks = 2 * (45 + 27)
     factors = 3 * (45 + 81)
     return N * w * (stage + state + sblocks + factors) * ipm_iters_total
+
+
+def file_sha16(path):
+    try:
+        return hashlib.sha256(open(path, 'rb').read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
+def pmc_traffic(kernel, lib_path):
+    """HBM bytes per QP launch from profiles/qp_pmc_traffic.json (rocprofv3 FETCH_SIZE / WRITE_SIZE
+    passes on the metric config, scripts/gpu_profile.sh) with its provenance: the git head and the
+    library it was measured with, and whether that library is the one loaded now."""
+    pmc = os.path.join(ROOT, 'profiles', 'qp_pmc_traffic.json')
+    if not os.path.exists(pmc):
+        return None, None
+    try:
+        d = json.load(open(pmc))
+    except Exception:
+        return None, None
+    lib = file_sha16(lib_path)
+    prov = {'file': 'profiles/qp_pmc_traffic.json', 'head': d.get('head'), 'command': d.get('command'),
+            'lib_sha16': d.get('lib_sha16'), 'loaded_lib_sha16': lib,
+            'same_library': d.get('lib_sha16') is not None and d.get('lib_sha16') == lib,
+            'kernel': d.get('kernel')}
+    return d.get('hbm_bytes_per_launch'), prov
 
 
 def cpu_info():
@@ -261,6 +291,11 @@ def main():
     ipm_total = solver.qp_iterations_total()        # IPM iterations of the last step, all problems
     _, _, qst, _ = solver.qp_solution(with_y=False)
     merit, nref = solver.qp_info()
+    rep_ms = []
+    if not args.no_extras:   # SURVEY.md 8d's median of 5, beside the contract's single timed region
+        for _ in range(5):
+            el, _ = timed_steps(solver, comm, args.steps)
+            rep_ms.append(el / args.steps * 1e3)
     gather_ms = None
     if comm is not None:   # the accepted solutions of every slice to rank 0 (uneven slices padded)
         comm.barrier()
@@ -273,14 +308,11 @@ def main():
     qp_mean_s = tim['qp_ms'] / 1e3 / n_steps
     achieved = algorithmic_qp_bytes(args.N, ipm_total, w, pb.robot) / qp_mean_s / 1e9
     compulsory = compulsory_qp_bytes(args.N, ipm_total, w, pb.robot) / qp_mean_s / 1e9
-    traffic = None
-    pmc = os.path.join(ROOT, 'profiles', 'qp_pmc_traffic.json')
+    traffic, traffic_prov = None, None
     metric_config = (args.config, args.N, nb, w) == ('trot', 100, 1024, 8)
-    if metric_config and os.path.exists(pmc):   # the PMC summary was measured on the metric config only
-        try:
-            traffic = json.load(open(pmc)).get('hbm_bytes_per_launch')
-        except Exception:
-            traffic = None
+    if metric_config:   # the PMC summary was measured on the metric config only
+        from cmpc import _lib as L
+        traffic, traffic_prov = pmc_traffic(solver.qp_kernel(), L.LIB_PATH)
     u, c = np.unique(qst, return_counts=True)
     out = {
         'metric': METRIC,
@@ -306,7 +338,9 @@ def main():
                     'refine_steps': int(nref.sum())},
         'roofline': {'kernel': solver.qp_kernel(), 'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                      'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
+                     'traffic_provenance': traffic_prov,
                      'compulsory': {'achieved': compulsory, 'frac': compulsory / HBM_PEAK_GBS}},
+        'repeats': {'ms_per_step': rep_ms, 'median_ms_per_step': float(np.median(rep_ms)) if rep_ms else None},
     }
     if gather_ms is not None:
         out['gather_ms'] = gather_ms
@@ -325,8 +359,10 @@ def main():
             s2.close()
             out[other + '_scaling'] = {'global_batch': units2, 'per_gpu': nb2,
                                        'value': units2 * args.steps / el2, 'ms_per_step': el2 / args.steps * 1e3}
-        # early exit, the reference's loop semantics, device-resident inputs, outputs copied back
-        solver.upload(pb, set_params=comm is None)
+        # early exit, the reference's loop semantics, device-resident inputs, outputs copied back: a
+        # batch this handle never solved (other seeds), so its first QP launch has no Newton counts
+        fresh = make_problems(args.config, args.N, nb, 10 ** 6 + lo)
+        solver.upload(fresh, set_params=comm is None)
         solver.solution(pinned=True)     # page-lock the output arrays and size the staging once, untimed
         solver.prefetch_ks()             # K, Sigma stream to the host behind the QP (quirk Q1: final early)
         solver.synchronize()
@@ -348,9 +384,10 @@ def main():
         out['early_exit'] = {'value': iters_all / dt_ee, 'unit': 'SCP iterations/s', 'ms': dt_ee * 1e3,
                              'scp_iterations': iters_all, 'loop_launches': int(n_loop),
                              'accepted': int((sol['n_accepted'] > 0).sum()),
-                             'note': 'solve_scp until every problem leaves the loop + D2H of X, U, K, Sigma '
-                                     '(fp64, reference layouts) into page-locked host arrays; K and Sigma '
-                                     'stream during the solve (cmpc_prefetch_ks)'}
+                             'note': 'a never-solved batch (seed offset 1e6): solve_scp until every problem '
+                                     'leaves the loop + D2H of X, U, K, Sigma (fp64, reference layouts) into '
+                                     'page-locked host arrays; K and Sigma stream during the solve '
+                                     '(cmpc_prefetch_ks)'}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out['cpu_baseline'] = cpu_baseline(args.N)

@@ -75,7 +75,7 @@ EXPORTS = ['cmpc_create', 'cmpc_destroy', 'cmpc_last_error', 'cmpc_version', 'cm
            'cmpc_get_solution', 'cmpc_get_iteration_log', 'cmpc_get_timing', 'cmpc_timing_begin',
            'cmpc_timing_end', 'cmpc_get_qp_iterations_total', 'cmpc_debug_stamps', 'cmpc_get_qp_kernel', 'cmpc_set_scp_mode',
            'cmpc_get_linearization_point', 'cmpc_interpolate', 'cmpc_generate_contact_plans',
-           'cmpc_upload_states', 'cmpc_get_contact_plans', 'cmpc_get_warm_start', 'cmpc_get_qp_info',
+           'cmpc_upload_states', 'cmpc_get_contact_plans', 'cmpc_get_warm_start', 'cmpc_get_qp_info', 'cmpc_get_qp_tail',
            'cmpc_comm_get_unique_id', 'cmpc_comm_init', 'cmpc_comm_destroy', 'cmpc_comm_bcast_params',
            'cmpc_comm_allreduce_max', 'cmpc_comm_gather_solution', 'cmpc_load_qp', 'cmpc_get_iteration_history',
            'cmpc_get_accepted', 'cmpc_host_register', 'cmpc_host_unregister',
@@ -136,6 +136,7 @@ def load():
         'cmpc_get_contact_plans': (i32, [h, vp, vp, vp]),
         'cmpc_get_warm_start': (i32, [h, vp, vp]),
         'cmpc_get_qp_info': (i32, [h, vp, vp]),
+        'cmpc_get_qp_tail': (i32, [h, vp]),
         'cmpc_comm_get_unique_id': (i32, [vp]),
         'cmpc_comm_init': (i32, [h, i32, i32, vp]),
         'cmpc_comm_destroy': (i32, [h]),
@@ -419,6 +420,13 @@ class Solver:
         merit = np.zeros(self.B); nref = np.zeros(self.B, np.int32)
         self._chk(self.lib.cmpc_get_qp_info(self.h, _ptr(merit), _ptr(nref)), 'cmpc_get_qp_info')
         return merit, nref
+
+    def qp_tail(self):
+        """Per problem, the Newton steps of the last QP that ran on the whole grouped workgroup after
+        the hand-over (0: solved on its own wave only)."""
+        out = np.zeros(self.B, np.int32)
+        self._chk(self.lib.cmpc_get_qp_tail(self.h, _ptr(out)), 'cmpc_get_qp_tail')
+        return out
 
     def solution(self, pinned=False, with_ks=True):
         """Accepted X, U (and with_ks K, Sigma) plus the per-problem SCP state.  pinned=True writes

@@ -28,13 +28,14 @@ ID_BYTES = 128
 
 
 def shard_bounds(B, rank, world):
-    """[lo, hi) of rank's contiguous slice: ceil(B / world) problems per rank, the last ranks
-    possibly short or empty."""
+    """[lo, hi) of rank's contiguous slice: floor(B / world) or ceil(B / world) problems per rank
+    (the first B % world ranks one more), so no rank is empty while B >= world (an empty rank could
+    not join the gather collective, csrc/comm.cpp).  B = 1024 over 1/2/4/8 ranks: equal slices."""
     if world < 1 or not 0 <= rank < world:
         raise ValueError('invalid rank %d of %d' % (rank, world))
-    per = -(-B // world)
-    lo = min(B, rank * per)
-    return lo, min(B, lo + per)
+    if B < world:
+        raise ValueError('batch %d < %d ranks: a rank would hold no problem' % (B, world))
+    return rank * B // world, (rank + 1) * B // world
 
 
 def world_from_env():

@@ -22,9 +22,9 @@ template <typename T, int R> __global__ void k_lin_knots(DevBuf<T>, int, int);
 template <typename T, int R> __global__ void k_cov_scan(DevBuf<T>, int);
 template <typename T, int R, bool FULL> __global__ void k_assemble(DevBuf<T>, int);
 template <typename T, int R, int NTT> __global__ void k_qp_ipm(DevBuf<T>, int, int, T, T, T, T, T);
-template <typename T, int R, int P, int W> __global__ void k_qp_group(DevBuf<T>, const int *, int, int, int, T, T, T, T, T);
+template <typename T, int R, int P> __global__ void k_qp_group(DevBuf<T>, const int *, int, int, int, T, T, T, T, T);
 template <typename T> __global__ void k_qp_order(DevBuf<T>, int, int, int *);
-size_t ipm_group_lds_bytes(int N, int prec_bytes, int P, int W);
+size_t ipm_group_lds_bytes(int N, int prec_bytes, int P);
 int ipm_pair_max_batch();
 template <typename T> __global__ void k_interpolate(DevBuf<T>, int, int, T *, T *);
 template <typename T, int R> __global__ void k_contact_plan(DevBuf<T>, const cmpc_gait *, const T *, uint8_t *, T *, T *);
@@ -105,48 +105,44 @@ template <typename T> DevParams<T> conv_params(const cmpc_params &p, int nw) {
 // more than one pass of 64 knots
 // Four waves (schur_pt.hpp: the Schur recurrence as four chains) when every problem still gets a
 // CU of its own and the horizon gives each chain a few blocks.
+// The four chains need N >= 16 (pt_seps gives every chain a few blocks), so a request for four waves
+// on a shorter horizon gets two, from the setting and from the diagnostic override alike.
 int qp_waves(cmpc_handle h) {
+    auto fit = [&](int w) { return w == 4 && h->N < 16 ? 2 : w; };
     if (const char *e = std::getenv("CMPC_QP_WAVES")) {   // diagnostic override (timing experiments)
         const int w = std::atoi(e);
-        if (w == 1 || w == 2 || w == 4) return w;
+        if (w == 1 || w == 2 || w == 4) return fit(w);
     }
-    if (h->qs.waves_per_problem > 0) return h->qs.waves_per_problem == 4 && h->N < 16 ? 2 : h->qs.waves_per_problem;
+    if (h->qs.waves_per_problem > 0) return fit(h->qs.waves_per_problem);
     if (h->N >= 40 && (long)h->B <= (long)h->n_cu) return 4;
     return (h->N + 1 > 64 && 2L * h->B <= 4L * h->n_cu) ? 2 : 1;
 }
 
 // Grouped QP workgroups (k_qp_group: P problems per P-wave workgroup, one per wave, all P waves on
-// the last one once the others have finished) in place of one wave per problem, for fp64 batches
+// the last one once the others have stopped) in place of one wave per problem, for fp64 batches
 // that fit k_qp_order: four problems per workgroup where the four-chain recurrence applies (N >= 40)
 // and four regions fit a CU's LDS, else two.  Same-box A/B (profiles/r03c_pair_ab.log): pairs took
 // the metric config's QP from 2.93 to 2.75 ms; BASELINE C3 (fp32, two Newton steps, no tail to
-// balance) 0.744 -> 0.752 ms, so fp32 keeps one wave per problem.  Diagnostics: CMPC_QP_PAIR=0
-// turns grouping off, =2 keeps the groups but never shares a problem; CMPC_QP_GROUP=2|4 forces the
-// group size.  Returns P, or 0 for one wave per problem.
-int qp_group(cmpc_handle h, int *waves = nullptr) {
+// balance) 0.744 -> 0.752 ms, so fp32 keeps one wave per problem.  Two two-wave problems per
+// four-wave workgroup (round 3, k_qp_group<.., 2, 2>) were a measured wash on the 512-problem
+// shard and -4% on C4 (profiles/r03g_group2w_ab.log): gfx950 has no half-workgroup barrier, and the
+// LDS spin barrier that stood in for it cost what the tail gained; removed in round 4.
+// Diagnostics: CMPC_QP_PAIR=0 turns grouping off, =2 keeps the groups but never shares a problem;
+// CMPC_QP_GROUP=2|4 forces the group size.  Returns P, or 0 for one wave per problem.
+int qp_group(cmpc_handle h) {
     const int w = qp_waves(h);
-    if (waves) *waves = w;
-    if ((w != 1 && w != 2) || h->B < 2 || h->B > ipm_pair_max_batch() || h->prec != CMPC_PREC_F64) return 0;
+    if (w != 1 || h->B < 2 || h->B > ipm_pair_max_batch() || h->prec != CMPC_PREC_F64) return 0;
     if (const char *e = std::getenv("CMPC_QP_PAIR"))
         if (e[0] == '0') return 0;
     const size_t cap = 160 * 1024 - 1024;
     const int esz = (int)h->esz();
-    if (w == 2) {   // two two-wave problems, the last on four waves (four chains: N >= 40)
-        // Off unless CMPC_QP_GROUP2W=1: the two-wave loop's ~25 barriers per Newton step become LDS
-        // spin barriers (gsync<128, 256>), which cost the 512-problem shard what the tail gains
-        // (same-box: unshared groups 1.74 -> 1.86 ms, sharing back to 1.74 ms; C4 54.1k -> 51.7k SCP
-        // it/s: profiles/r03g_group2w_ab.log)
-        const char *e = std::getenv("CMPC_QP_GROUP2W");
-        if (!(e && e[0] == '1')) return 0;
-        return h->N >= 40 && ipm_group_lds_bytes(h->N, esz, 2, 2) <= cap ? 2 : 0;
-    }
-    int P = h->N >= 40 && ipm_group_lds_bytes(h->N, esz, 4, 1) <= cap ? 4 : 2;
+    int P = h->N >= 40 && ipm_group_lds_bytes(h->N, esz, 4) <= cap ? 4 : 2;
     if (const char *e = std::getenv("CMPC_QP_GROUP")) {
         if (e[0] == '2') P = 2;
         if (e[0] == '4' && h->N >= 40) P = 4;
     }
-    if (ipm_group_lds_bytes(h->N, esz, P, 1) > cap) P = 2;
-    return ipm_group_lds_bytes(h->N, esz, P, 1) <= cap ? P : 0;
+    if (ipm_group_lds_bytes(h->N, esz, P) > cap) P = 2;
+    return ipm_group_lds_bytes(h->N, esz, P) <= cap ? P : 0;
 }
 
 // CMPC_QP_PAIR=2: grouped workgroups whose waves never share a problem (diagnostic: the cost of the
@@ -259,12 +255,10 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
         // (N+2) x 9 Schur vector and the sweep rings in LDS, the Schur blocks in the workspace
         const int nt = 64 * qp_waves(h);
         const T eta = T(qp_step_fraction(h));
-        int gw = 1;
-        if (const int P = qp_group(h, &gw)) {
-            const size_t lds = ipm_group_lds_bytes(h->N, (int)sizeof(T), P, gw);
-            const void *fn = gw == 2 ? reinterpret_cast<const void *>(&k_qp_group<T, R, 2, 2>)
-                             : P == 4 ? reinterpret_cast<const void *>(&k_qp_group<T, R, 4, 1>)
-                                      : reinterpret_cast<const void *>(&k_qp_group<T, R, 2, 1>);
+        if (const int P = qp_group(h)) {
+            const size_t lds = ipm_group_lds_bytes(h->N, (int)sizeof(T), P);
+            const void *fn = P == 4 ? reinterpret_cast<const void *>(&k_qp_group<T, R, 4>)
+                                    : reinterpret_cast<const void *>(&k_qp_group<T, R, 2>);
             HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
             if (h->scan_deferred) {   // the scans run in the QP's waves
                 HIPCHK(hipMemsetAsync(h->scan_ctr, 0, sizeof(unsigned), h->stream));
@@ -273,16 +267,12 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
             }
             hipLaunchKernelGGL((k_qp_order<T>), dim3(1), dim3(1024), 0, h->stream, d, only_active, P, (int *)h->qp_order);
             const unsigned ng = (unsigned)((B + P - 1) / P);
-            if (gw == 2)
-                hipLaunchKernelGGL((k_qp_group<T, R, 2, 2>), dim3(ng), dim3(256), lds, h->stream, d, (const int *)h->qp_order,
-                                   only_active, qp_pair_share(), h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), eta,
-                                   T(h->qs.init_floor_s), T(h->qs.init_floor_l));
-            else if (P == 4)
-                hipLaunchKernelGGL((k_qp_group<T, R, 4, 1>), dim3(ng), dim3(256), lds, h->stream, d, (const int *)h->qp_order,
+            if (P == 4)
+                hipLaunchKernelGGL((k_qp_group<T, R, 4>), dim3(ng), dim3(256), lds, h->stream, d, (const int *)h->qp_order,
                                    only_active, qp_pair_share(), h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), eta,
                                    T(h->qs.init_floor_s), T(h->qs.init_floor_l));
             else
-                hipLaunchKernelGGL((k_qp_group<T, R, 2, 1>), dim3(ng), dim3(128), lds, h->stream, d, (const int *)h->qp_order,
+                hipLaunchKernelGGL((k_qp_group<T, R, 2>), dim3(ng), dim3(128), lds, h->stream, d, (const int *)h->qp_order,
                                    only_active, qp_pair_share(), h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), eta,
                                    T(h->qs.init_floor_s), T(h->qs.init_floor_l));
             if (h->scan_pending) {
@@ -568,6 +558,10 @@ void reset_scp(cmpc_handle h, const int32_t *class_id) {
         st[b] = s;
     }
     HIPCHK(hipMemcpyAsync(h->scp, st.data(), st.size() * sizeof(ScpState), hipMemcpyHostToDevice, h->stream));
+    // a new batch has no Newton-step counts: the first grouped QP launch orders its problems by
+    // index (k_qp_order), not by counts learned on whatever the handle solved before
+    HIPCHK(hipMemsetAsync(h->qp_iters, 0, (size_t)h->B * 4, h->stream));
+    HIPCHK(hipMemsetAsync(h->qp_tail, 0, (size_t)h->B * 4, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
 }
 
@@ -679,6 +673,7 @@ int cmpc_create(cmpc_handle *out, int device, int robot, int N, int max_batch, i
         h->qp_iters = h->dalloc(Bm * 4);
         h->qp_merit = h->dalloc(Bm * e);
         h->qp_nref = h->dalloc(Bm * 4);
+        h->qp_tail = h->dalloc(Bm * 4);
         h->ws_stride = ipm_workspace_elems(N, robot);
         h->ws = h->dalloc(Bm * h->ws_stride * e);
         h->scp = h->dalloc(Bm * sizeof(ScpState));
@@ -1194,6 +1189,14 @@ int cmpc_get_qp_info(cmpc_handle h, double *merit, int32_t *n_refine) {
     });
 }
 
+int cmpc_get_qp_tail(cmpc_handle h, int32_t *tail_steps) {
+    return guard(h, [&] {
+        need(h->B > 0, "no problems uploaded");
+        need(tail_steps != nullptr, "null output buffer");
+        from_dev_raw(h, tail_steps, h->qp_tail, (size_t)h->B * 4);
+    });
+}
+
 int cmpc_get_solution(cmpc_handle h, double *X, double *U, double *K, double *Sigma, int32_t *n_accepted,
                       int32_t *iterations, int32_t *scp_status, double *weight, double *radius) {
     return guard(h, [&] {
@@ -1415,9 +1418,8 @@ int cmpc_get_qp_iterations_total(cmpc_handle h, int64_t *total) {
 int cmpc_get_qp_kernel(cmpc_handle h, char *buf, int n) {
     return guard(h, [&] {
         need(buf != nullptr && n > 0, "null output");
-        int gw = 1;
-        const int P = qp_group(h, &gw);
-        const std::string s = P ? "k_qp_group<" + std::to_string(P) + "x" + std::to_string(gw) + ">"
+        const int P = qp_group(h);
+        const std::string s = P ? "k_qp_group<" + std::to_string(P) + ">"
                                 : "k_qp_ipm<" + std::to_string(qp_waves(h)) + ">";
         std::snprintf(buf, (size_t)n, "%s", s.c_str());
     });

@@ -88,6 +88,7 @@ template <typename T> struct DevBuf {
     int32_t *qp_status, *qp_iters;
     T *qp_merit;                    // (B) final merit (residual / tolerance; <= 1 when solved)
     int32_t *qp_nref;               // (B) refinement steps taken
+    int32_t *qp_tail;               // (B) Newton steps run on the whole workgroup after a hand-over (k_qp_group)
     // IPM workspace
     T *ws;
     size_t ws_stride;               // elements per problem
@@ -148,33 +149,14 @@ template <typename T> __device__ __forceinline__ T wave_sum(T v) {
 // G | WG, groups aligned to G): the workgroup barrier when the group is the workgroup; a wave-level
 // barrier with workgroup-scope fences (the same waits on LDS and global memory as __syncthreads,
 // without the s_barrier the other waves of the workgroup are not part of) when it is one wave of
-// a larger workgroup (k_qp_pair: one problem per wave until one of them has finished).
-// Two-wave groups of a four-wave workgroup (k_qp_group<.., 2, 2>) have no hardware barrier of their
-// own: word 2 g of cmpc_hbar counts the group's arrivals (two per barrier).  The workgroup zeroes
-// the words before its groups start.
-static __shared__ int cmpc_hbar[4];
-
+// a larger workgroup (k_qp_group: one problem per wave until the last one is handed over).
 template <int G, int WG> __device__ __forceinline__ void gsync() {
-    static_assert(G == WG || G == 64 || (G == 128 && WG == 256), "a group is the workgroup, one of its waves, or half of four");
+    static_assert(G == WG || G == 64, "a group is the workgroup or one of its waves");
     if constexpr (G == WG) {
         __syncthreads();
-    } else if constexpr (G == 64) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     } else {
-        using LdsI = __attribute__((address_space(3))) int;
-        LdsI *ctr = (LdsI *)cmpc_hbar + 2 * (threadIdx.x >> 7);   // ds_* instructions, not flat ones
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
-        int old = 0;
-        if ((threadIdx.x & 63) == 0) old = __atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED);
-        old = __builtin_amdgcn_readfirstlane(__shfl(old, 0, 64));
-        // the arrivals count rises by two per barrier: the first wave in (even count) waits until
-        // the second one has added its arrival
-        if (!(old & 1))
-            while (__builtin_amdgcn_readfirstlane(*(volatile LdsI *)ctr) < old + 2) {
-            }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
 }

@@ -2064,10 +2064,13 @@ __device__ __forceinline__ T refine_direction(const Ctx<T, ROBOT> &C, T sigma_mu
 // direction) split each knot into a state part (waves 0, 1) and a contact part (waves 2, 3).
 template <int G> constexpr bool split_knots() { return G >= 256; }
 
-// Newton-loop state of one problem's solve (carried across k_qp_group's change of mode)
+// Newton-loop state of one problem's solve (carried across k_qp_group's change of mode).  A solve
+// handed over after the stopping test of iteration `it` (yielded) resumes there on all waves: the
+// residual pass of that iteration is done (its outputs are in the workspace), and mu / cnt are its
+// complementarity mean and row count.
 template <typename T> struct IpmState {
-    int status, it, stall, n_refine, yielded;
-    T mu_prev, merit, prim_prev;
+    int status, it, stall, n_refine, yielded, resume, tail;
+    T mu_prev, merit, prim_prev, mu, cnt;
 #ifdef CMPC_STAMPS
     unsigned long long t_acc[12];
 #endif
@@ -2075,9 +2078,9 @@ template <typename T> struct IpmState {
 template <typename T> __device__ __forceinline__ IpmState<T> ipm_state0() {
     IpmState<T> S;
     S.status = CMPC_QP_MAX_ITER;
-    S.it = S.stall = S.n_refine = S.yielded = 0;
+    S.it = S.stall = S.n_refine = S.yielded = S.resume = S.tail = 0;
     S.mu_prev = T(-1);
-    S.merit = S.prim_prev = T(0);
+    S.merit = S.prim_prev = S.mu = S.cnt = T(0);
 #ifdef CMPC_STAMPS
     for (int i = 0; i < 12; ++i) S.t_acc[i] = 0;
 #endif
@@ -2155,13 +2158,47 @@ __device__ __forceinline__ void ipm_start(const DevBuf<T> &d, const Ctx<T, ROBOT
     gsync<G, WG>();
 }
 
+// Hand-over of a grouped problem (k_qp_group), decided by the problems' Newton-step counts only,
+// never by timing.  gf: per wave of the workgroup, cont[w] (gf[w]) = the last iteration whose
+// stopping test let wave w's problem continue, done[w] (gf[4 + w]) = 1 once it has left its loop
+// (cont frozen).  After its own stopping test of iteration `it` let it continue, a wave publishes
+// cont[w] = it and asks whether every other problem of the group finished by iteration `it` (done
+// with cont < it).  It waits only for problems whose status at `it` is not yet published, and only
+// while none is known to continue (cont >= it); every wave publishes before it waits, so no two
+// waves wait on each other.  So the last problem is handed over right after the stopping test of
+// the iteration in which the slowest other problem stopped, whatever the waves' relative speed:
+// results are bit-reproducible (tests/test_gpu_qp_pair.py).  The spin is bounded (~60 ms); past it
+// the problem just finishes on its own wave (correct, only slower).
+__device__ __forceinline__ bool group_handover(LdsT<int> *gf, int P, int w, int it) {
+    volatile LdsT<int> *cont = gf, *done = gf + 4;
+    if ((threadIdx.x & 63) == 0) cont[w] = it;
+    for (int spin = 0; spin < (1 << 20); ++spin) {
+        bool any_cont = false, unknown = false;
+        for (int q = 0; q < P; ++q) {
+            if (q == w) continue;
+            const int dq = __builtin_amdgcn_readfirstlane(done[q]);   // done before cont: cont is
+            const int cq = __builtin_amdgcn_readfirstlane(cont[q]);   // final once done reads 1
+            if (cq >= it) any_cont = true;
+            else if (!dq) unknown = true;
+        }
+        if (any_cont) return false;
+        if (!unknown) return true;
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return false;
+}
+__device__ __forceinline__ void group_done(LdsT<int> *gf, int w) {
+    if ((threadIdx.x & 63) == 0) ((volatile LdsT<int> *)gf)[4 + w] = 1;
+}
+
 // Newton iterations of problem b on a group of G threads (the workgroup, or one wave of a WG-thread
-// workgroup), from S.it until the stopping test, a failure exit or the cap; with `yield` set, the
-// loop also leaves (S.yielded) once *yield (the workgroup's count of free waves) reaches yield_at.
+// workgroup), from S.it until the stopping test, a failure exit or the cap (S.resume: from after the
+// stopping test of S.it).  With gf set (k_qp_group, one wave per problem), the loop also leaves
+// (S.yielded) when group_handover hands the problem to the whole workgroup.
 template <typename T, int ROBOT, int G, int WG>
 __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT> &C, int b, IpmState<T> &S,
                                          const IpmLds<T> &L, int max_iter, T eps_abs, T eps_rel, T eta,
-                                         const volatile LdsT<int> *yield, int yield_at = 1) {
+                                         LdsT<int> *gf = nullptr, int gP = 0) {
     const int tid = threadIdx.x & (G - 1), N = C.N, K1 = N + 1, NB = N + 2, NBm = NB / 2;
     (void)b;
 #ifdef CMPC_STAMPS
@@ -2177,28 +2214,19 @@ __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT>
 #endif
     int status = S.status, it = S.it, stall = S.stall, n_refine = S.n_refine;
     T mu_prev = S.mu_prev, merit = S.merit, prim_prev = S.prim_prev;
-    // k_qp_group: have the other problems of the workgroup finished?  A group of two waves decides
-    // once for both (its first thread reads the count and publishes it behind the group barrier),
-    // so its waves never part ways
-    auto want_yield = [&]() -> bool {
-        if (!yield) return false;
-        if constexpr (G > 64 && G < WG) {
-            if (tid == 0) L.red[31] = T(__builtin_amdgcn_readfirstlane(*yield) >= yield_at ? 1 : 0);
-            gsync<G, WG>();
-            return L.red[31] != T(0);
-        } else {
-            return __builtin_amdgcn_readfirstlane(*yield) >= yield_at;
-        }
-    };
+    bool resume = S.resume != 0;
+    S.resume = 0;
     // it == 0 is the initialization step: one full Newton step from s = lambda = 1 gives an
     // equality-feasible least-squares start; s and lambda are then floored row by row (Solo12)
     // or shifted by 1 + the largest violation (TALOS), see init_s_knot.
     for (it = S.it; it <= max_iter; ++it) {
-        // k_qp_group: the other waves have finished, so this problem continues on all of them
-        if (want_yield()) { S.yielded = 1; break; }
         const bool init = (it == 0);
-        const int stall0 = stall;
-        const T mu_prev0 = mu_prev, prim_prev0 = prim_prev;
+        T mu, cnt;   // complementarity mean and row count of this iteration's residual pass
+        if (resume) {   // handed over after this iteration's stopping test (k_qp_group)
+            resume = false;
+            mu = S.mu;
+            cnt = S.cnt;
+        } else {
         Norms<T, ROBOT> nm{0, 0, 0, 0, 0, 0, 0, 0};
         if constexpr (split_knots<G>()) {   // a thread pair per knot: state part | contact part
             // (the part is the wave's: a uniform branch)
@@ -2216,7 +2244,8 @@ __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT>
         block_reduce<T, G, 2, 0, WG>(sm2, L.red);
         STAMP(0);
         const T prim = mx[0], dual = mx[1], comp = mx[2], sp = mx[3], sdd = mx[4];
-        const T mu = sm2[0] / fmax(sm2[1], T(1));
+        mu = sm2[0] / fmax(sm2[1], T(1));
+        cnt = sm2[1];
         const T ep = eps_abs + eps_rel * sp, ed = eps_abs + eps_rel * sdd;
         merit = fmax(prim / ep, fmax(dual / ed, comp / ed));
         if (!(merit == merit) || !(mu == mu)) { status = CMPC_QP_NONFINITE; break; }
@@ -2243,21 +2272,16 @@ __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT>
             if (stall >= 3 && merit <= T(1e3)) { status = CMPC_QP_SOLVED_INACCURATE; break; }
         }
         if (it == max_iter) break;
-        // The partner may finish while this iteration runs (both problems start together, so it
-        // detects convergence in the same residual pass).  Nothing of the iterate changes before
-        // the update, so up to the S blocks the loop can still leave and let the two-wave loop
-        // redo the iteration from its top, with the stopping-test state it started from: at about
-        // 0.57 of the one-wave time per Newton step, redoing beats finishing the iteration alone
-        // while less than ~40% of it is done (residual 19%, Phi factors and w 10%, S blocks 4%).
-        auto leave = [&]() {
-            if (!want_yield()) return false;
+        // k_qp_group: every other problem of the workgroup has stopped, so this one continues on
+        // all waves from here (the residual pass of this iteration is in the workspace)
+        if (gf && group_handover(gf, gP, (int)(threadIdx.x >> 6), it)) {
             S.yielded = 1;
-            stall = stall0;
-            mu_prev = mu_prev0;
-            prim_prev = prim_prev0;
-            return true;
-        };
-        if (leave()) break;
+            S.resume = 1;
+            S.mu = mu;
+            S.cnt = cnt;
+            break;
+        }
+        }   // (residual pass and stopping test)
         // ---- Phi factors and the predictor's particular solution (knot-local), then the S blocks
         // and the predictor's Schur right-hand side
         if constexpr (split_knots<G>()) {
@@ -2286,12 +2310,10 @@ __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT>
         }
         gsync<G, WG>();
         STAMP(1);
-        if (leave()) break;
         if (G > 64) add_wx<T, G>(C.vb, C.wxs, N, C.bus);
         for (int k = tid; k < K1; k += G) phase_sblock<T, ROBOT>(C, k);
         gsync<G, WG>();
         STAMP(2);
-        if (leave()) break;
         // ---- factorization of S with the predictor's forward elimination fused in
 #ifdef CMPC_STAMPS
         unsigned long long *fst = d.stamps + (size_t)b * 16;
@@ -2368,7 +2390,7 @@ __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT>
             if (init) break;
             if (corr == 0) {   // Mehrotra centering from the affine step's complementarity
                 block_reduce<T, G, 3, 0, WG>(mus, L.red);
-                const T mu_aff = (mus[0] + alpha * (mus[1] + alpha * mus[2])) / fmax(sm2[1], T(1));
+                const T mu_aff = (mus[0] + alpha * (mus[1] + alpha * mus[2])) / fmax(cnt, T(1));
                 const T sg = mu_aff / fmax(mu, std::numeric_limits<T>::min());
                 sigma_mu = sg * sg * sg * mu;
             } else if ((alpha < T(QP_REFINE_ALPHA) || stall > 0) && merit < T(QP_REFINE_MERIT)) {
@@ -2430,6 +2452,7 @@ __device__ __forceinline__ void ipm_finish(const DevBuf<T> &d, const Ctx<T, ROBO
         d.qp_iters[b] = S.it;
         d.qp_merit[b] = S.merit;
         d.qp_nref[b] = S.n_refine;
+        d.qp_tail[b] = S.tail;
 #ifdef CMPC_STAMPS
         for (int i = 0; i < 9; ++i) d.stamps[(size_t)b * 16 + i] = S.t_acc[i];   // 9..11: k_linearize, 12..15: tw_factor_ends
 #endif
@@ -2502,91 +2525,82 @@ __global__ void __launch_bounds__(NTT, NTT == 128 ? QP_MIN_WAVES_2W : QP_MIN_WAV
 // Batches of one wave per problem (the metric config: 1024 problems, one per SIMD) last as long as
 // their slowest problem: trot N=100 x 1024 takes 4 to 7 Newton steps per problem, so the SIMD of a
 // 4-step problem idles for three steps.  k_qp_group holds P problems per P-wave workgroup, one per
-// wave (the one-wave algorithm, ipm_loop<.., 64, 64 P>); once all but one have finished, the last
-// one leaves its loop (at the top of an iteration, or redoing the current one) and all P waves
-// finish it: with the two-wave algorithm (P = 2: one knot per thread, one end of the Schur
-// recurrence per wave) or the four-wave one (P = 4: four chains around three separators,
-// schur_pt.hpp).  k_qp_order puts the problems that took the most Newton steps in the previous
-// launch with those that took the fewest (inactive problems count zero).
+// wave (the one-wave algorithm, ipm_loop<.., 64, 64 P>); once all but one have stopped, the last
+// one is handed over (group_handover: right after the stopping test of the iteration in which the
+// slowest other problem stopped, so the hand-over point depends on Newton-step counts, never on
+// timing) and all P waves finish it from there: with the two-wave algorithm (P = 2: one knot per
+// thread, one end of the Schur recurrence per wave) or the four-wave one (P = 4: four chains
+// around three separators, schur_pt.hpp).  k_qp_order puts the problems that took the most Newton
+// steps in the previous launch with those that took the fewest (inactive problems count zero).
 //
 // LDS of one wave's problem (elements of T): Schur vector | two sweep rings (the two halves of
 // the wave) | recurrence scratch of the two ends | reductions | cost weights | contact masks.  When
 // all waves finish the last problem, it keeps its region; the other regions hold the w_x side
 // array and (P = 4) the fill products in their Schur-vector slots, and each wave uses its own
 // region's first ring and recurrence scratch.
-template <typename T, int W = 1> struct GroupLds {
-    // W = 2: the problem's w_x side array after its Schur vector; recurrence scratch for two
-    // four-chain waves (the last problem's four waves use both regions' scratch and rings)
-    static constexpr int RING = 2 * SWEEP_LDS, SH = W == 1 ? 2 * TW_SCRATCH : 2 * PT_SCRATCH, RED = 32, WTS = 48;
+template <typename T> struct GroupLds {
+    static constexpr int RING = 2 * SWEEP_LDS, SH = 2 * TW_SCRATCH, RED = 32, WTS = 48;
     static constexpr int CMS = (KPC + 8 * (int)sizeof(T) - 1) / (8 * (int)sizeof(T)) * 8;
-    static_assert(SH >= PT_SCRATCH * W && SH >= 2 * TW_SCRATCH, "a region holds its waves' recurrence scratch");
-    static_assert(W == 1 || SCAN_LDS <= 2 * SWEEP_LDS, "a wave's half of a region holds a covariance scan");
+    static_assert(SH >= PT_SCRATCH, "a region holds a four-chain wave's recurrence scratch");
     __host__ __device__ static constexpr int vec(int N) { return ((N + 2) * 9 + 7) & ~7; }
-    __host__ __device__ static constexpr int region(int N) { return W * vec(N) + RING + SH + RED + WTS + CMS; }
+    __host__ __device__ static constexpr int region(int N) { return vec(N) + RING + SH + RED + WTS + CMS; }
 };
 
-// P problems of W waves each per workgroup (WG = 64 P W threads): P = 2 or 4 with W = 1, or P = 2
-// with W = 2 (the 512-problem shards: two two-wave problems, the last one on all four waves; its
-// waves synchronize through the LDS barrier of gsync<128, 256>).
-template <typename T, int ROBOT, int P, int W>
-__global__ void __launch_bounds__(64 * P * W, 1) k_qp_group(DevBuf<T> d, const int *order, int only_active, int share,
-                                                            int max_iter, T eps_abs, T eps_rel, T eta, T floor_s,
-                                                            T floor_l) {
+// P problems per P-wave workgroup (P = 2 or 4), one per wave until the hand-over.
+template <typename T, int ROBOT, int P>
+__global__ void __launch_bounds__(64 * P, 1) k_qp_group(DevBuf<T> d, const int *order, int only_active, int share,
+                                                        int max_iter, T eps_abs, T eps_rel, T eta, T floor_s,
+                                                        T floor_l) {
     extern __shared__ __attribute__((aligned(16))) unsigned char dsmem[];
-    using GL = GroupLds<T, W>;
-    constexpr int G = 64 * W, WG = G * P;
-    static_assert(WG == 128 || WG == 256, "two or four waves per workgroup");
-    __shared__ int nfree, rem;
+    using GL = GroupLds<T>;
+    constexpr int WG = 64 * P;
+    static_assert(P == 2 || P == 4, "two or four waves per workgroup");
+    __shared__ int rem, gflags[8];   // gflags: cont[4] | done[4] (group_handover)
     __shared__ IpmState<T> Ss;
-    __shared__ T sbv_s[WG >= 256 ? 6 * 9 : 1];
-    const int w = threadIdx.x / G, lane = threadIdx.x & 63, N = d.N, NB = N + 2;
-    const int RG = GL::region(N), vec = GL::vec(N);
+    __shared__ T sbv_s[P == 4 ? 6 * 9 : 1];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, N = d.N, NB = N + 2;
+    const int RG = GL::region(N);
     LdsT<T> *base = (LdsT<T> *)reinterpret_cast<T *>(dsmem);
     auto region = [&](int v) { return base + (size_t)v * RG; };
-    auto after_vec = [&](LdsT<T> *R) { return R + W * vec; };
+    auto after_vec = [&](LdsT<T> *R) { return R + GL::vec(N); };
     auto wts_of = [&](LdsT<T> *R) { return after_vec(R) + GL::RING + GL::SH + GL::RED; };
     auto cms_of = [&](LdsT<T> *R) { return (LdsT<uint8_t> *)(after_vec(R) + GL::RING + GL::SH + GL::RED + GL::WTS); };
-    if (threadIdx.x == 0) {
-        nfree = 0;
-        rem = -1;
-        if (W == 2) for (int i = 0; i < 4; ++i) cmpc_hbar[i] = 0;
-    }
+    LdsT<int> *gf = (LdsT<int> *)gflags;
+    if (threadIdx.x == 0) rem = -1;
+    if (threadIdx.x < 8) gflags[threadIdx.x] = threadIdx.x < 4 ? -1 : 0;
     __syncthreads();
-    // one problem per group of W waves.  The problem index is the same on every lane of the wave:
-    // as a uniform (scalar) value, every pointer derived from it stays in SGPRs (as a per-lane value
-    // the one-wave mode spilled 888 B per lane and ran 11% slower than k_qp_ipm<.., 64>)
+    // one problem per wave.  The problem index is the same on every lane of the wave: as a uniform
+    // (scalar) value, every pointer derived from it stays in SGPRs (as a per-lane value the one-wave
+    // mode spilled 888 B per lane and ran 11% slower than k_qp_ipm<.., 64>)
     const int slot = P * blockIdx.x + w;
     const int b = __builtin_amdgcn_readfirstlane(slot < d.B ? order[slot] : -1);
-    const int gt = threadIdx.x & (G - 1);   // thread of the group
     if (b >= 0 && (!only_active || d.scp[b].active)) {
         LdsT<T> *R = region(w);
         Ctx<T, ROBOT> C{};
-        ctx_setup<T, ROBOT, G>(d, b, C, wts_of(R), cms_of(R), floor_s, floor_l);
-        gsync<G, WG>();
+        ctx_setup<T, ROBOT, 64>(d, b, C, wts_of(R), cms_of(R), floor_s, floor_l);
+        gsync<64, WG>();
         C.vb = R;
-        if (W == 2) C.wxs = R + vec;
         IpmLds<T> L;
-        L.ring = after_vec(R) + (lane >> 5) * SWEEP_LDS;   // the two ends' sweeps: halves of the group's first wave
+        L.ring = after_vec(R) + (lane >> 5) * SWEEP_LDS;   // the two ends' sweeps: halves of the wave
         L.shl = after_vec(R) + GL::RING;
         L.red = (T *)(after_vec(R) + GL::RING + GL::SH);
         IpmState<T> S = ipm_state0<T>();
-        ipm_start<T, ROBOT, G, WG>(d, C, b);
-        ipm_loop<T, ROBOT, G, WG>(d, C, b, S, L, max_iter, eps_abs, eps_rel, eta,
-                                  share ? (const volatile LdsT<int> *)&nfree : nullptr, P - 1);
+        ipm_start<T, ROBOT, 64, WG>(d, C, b);
+        ipm_loop<T, ROBOT, 64, WG>(d, C, b, S, L, max_iter, eps_abs, eps_rel, eta, share ? gf : nullptr, P);
         if (S.yielded) {
-            if (gt == 0) {
+            if (lane == 0) {
                 Ss = S;
                 rem = w;
             }
         } else {
-            if (gt == 0) atomicAdd(&nfree, 1);   // free: the last problem may leave its loop while
-            ipm_finish<T, ROBOT, G>(d, C, b, S); // this group writes the outputs (global memory only)
+            group_done(gf, w);                   // stopped: the last problem may be handed over
+            ipm_finish<T, ROBOT, 64>(d, C, b, S);   // while this wave writes the outputs (global memory only)
         }
-    } else if (gt == 0) {
-        atomicAdd(&nfree, 1);
+    } else {
+        group_done(gf, w);
     }
     __syncthreads();   // the first s_barrier of any wave since the start
-    // the last problem, if it left its loop, on all waves
+    // the last problem, if it was handed over, on all waves
     const int r = rem;
     if (r >= 0) {
         const int b2 = __builtin_amdgcn_readfirstlane(order[P * blockIdx.x + r]);
@@ -2597,26 +2611,18 @@ __global__ void __launch_bounds__(64 * P * W, 1) k_qp_group(DevBuf<T> d, const i
         C.vb = R;
         IpmLds<T> L;
         const int wv = threadIdx.x >> 6;
-        if constexpr (WG >= 256) {   // four waves: four chains, split knots
+        if constexpr (P == 4) {   // four waves: four chains, split knots; the other regions' Schur-vector
+                                  // slots, each wave its own region's ring and scratch
             C.Sh = C.ws + Ws<ROBOT>::Sh;
             C.Sx = C.ws + Ws<ROBOT>::Sx;
             pt_seps<T>(NB, C.sp);
             C.sbv = (LdsT<T> *)sbv_s;
-            if (W == 1) {   // the other regions' Schur-vector slots; each wave its own region's ring, scratch
-                C.wxs = region((r + 1) % P);
-                C.hy = region((r + 2) % P);
-                C.bus = region((r + 3) % P);
-                L.ring = after_vec(region(wv));
-                L.shl = after_vec(region(wv)) + GL::RING;
-            } else {        // R's w_x slot; the other region's two vector slots; wave v: ring and
-                            // scratch v % 2 of region v / 2
-                C.wxs = R + vec;
-                C.hy = region(1 - r);
-                C.bus = region(1 - r) + vec;
-                L.ring = after_vec(region(wv >> 1)) + (wv & 1) * SWEEP_LDS;
-                L.shl = after_vec(region(wv >> 1)) + GL::RING + (wv & 1) * PT_SCRATCH;
-            }
-        } else {   // two waves, pairs of one-wave problems: the ends' sweeps on the halves of wave 0
+            C.wxs = region((r + 1) % P);
+            C.hy = region((r + 2) % P);
+            C.bus = region((r + 3) % P);
+            L.ring = after_vec(region(wv));
+            L.shl = after_vec(region(wv)) + GL::RING;
+        } else {   // two waves: the ends' sweeps on the halves of wave 0
             C.wxs = region(1 - r);
             L.ring = after_vec(R) + (lane >> 5) * SWEEP_LDS;
             L.shl = after_vec(R) + GL::RING;
@@ -2624,11 +2630,12 @@ __global__ void __launch_bounds__(64 * P * W, 1) k_qp_group(DevBuf<T> d, const i
         L.red = (T *)(after_vec(R) + GL::RING + GL::SH);
         IpmState<T> S = Ss;
         S.yielded = 0;
+        const int it0 = S.it;
 #ifdef CMPC_STAMPS
         const unsigned long long tb0 = __builtin_amdgcn_s_memtime();
-        const int it0 = S.it;
 #endif
-        ipm_loop<T, ROBOT, WG, WG>(d, C, b2, S, L, max_iter, eps_abs, eps_rel, eta, nullptr);
+        ipm_loop<T, ROBOT, WG, WG>(d, C, b2, S, L, max_iter, eps_abs, eps_rel, eta);
+        S.tail = S.it - it0;
         ipm_finish<T, ROBOT, WG>(d, C, b2, S);
 #ifdef CMPC_STAMPS
         if (threadIdx.x == 0) {   // slots 9, 10: cycles and Newton steps on all waves
@@ -2640,7 +2647,7 @@ __global__ void __launch_bounds__(64 * P * W, 1) k_qp_group(DevBuf<T> d, const i
     // covariance scan jobs of a deterministic batch, each wave on its own (as in k_qp_ipm<.., 64>)
     if (d.scan_ctr) {
         __syncthreads();   // the dynamic LDS is free from here on
-        LdsT<T> *R = base + (size_t)(threadIdx.x >> 6) * (RG / W / 8 * 8);   // a slice per wave
+        LdsT<T> *R = base + (size_t)(threadIdx.x >> 6) * (RG / 8 * 8);   // a slice per wave
         for (;;) {
             int j = 0;
             if (lane == 0) j = (int)atomicAdd(d.scan_ctr, 1u);
@@ -2720,9 +2727,8 @@ template <typename T> __global__ void __launch_bounds__(1024) k_qp_order(DevBuf<
     template __global__ void k_qp_ipm<T, R, 64>(DevBuf<T>, int, int, T, T, T, T, T);     \
     template __global__ void k_qp_ipm<T, R, 128>(DevBuf<T>, int, int, T, T, T, T, T);    \
     template __global__ void k_qp_ipm<T, R, 256>(DevBuf<T>, int, int, T, T, T, T, T);    \
-    template __global__ void k_qp_group<T, R, 2, 1>(DevBuf<T>, const int *, int, int, int, T, T, T, T, T); \
-    template __global__ void k_qp_group<T, R, 4, 1>(DevBuf<T>, const int *, int, int, int, T, T, T, T, T); \
-    template __global__ void k_qp_group<T, R, 2, 2>(DevBuf<T>, const int *, int, int, int, T, T, T, T, T);
+    template __global__ void k_qp_group<T, R, 2>(DevBuf<T>, const int *, int, int, int, T, T, T, T, T); \
+    template __global__ void k_qp_group<T, R, 4>(DevBuf<T>, const int *, int, int, int, T, T, T, T, T);
 INST(double, 0)
 INST(double, 1)
 INST(float, 0)
@@ -2731,10 +2737,9 @@ INST(float, 1)
 template __global__ void k_qp_order<double>(DevBuf<double>, int, int, int *);
 template __global__ void k_qp_order<float>(DevBuf<float>, int, int, int *);
 
-// dynamic LDS of k_qp_group with P problems of W waves per workgroup
-size_t ipm_group_lds_bytes(int N, int prec_bytes, int P, int W) {
-    const size_t e = W == 1 ? (prec_bytes == 8 ? GroupLds<double, 1>::region(N) : GroupLds<float, 1>::region(N))
-                            : (prec_bytes == 8 ? GroupLds<double, 2>::region(N) : GroupLds<float, 2>::region(N));
+// dynamic LDS of k_qp_group with P problems per workgroup
+size_t ipm_group_lds_bytes(int N, int prec_bytes, int P) {
+    const size_t e = prec_bytes == 8 ? GroupLds<double>::region(N) : GroupLds<float>::region(N);
     return (size_t)P * e * prec_bytes;
 }
 int ipm_pair_max_batch() { return ORD_MAXB; }

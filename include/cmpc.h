@@ -220,6 +220,10 @@ int cmpc_get_qp_solution(cmpc_handle h, double *z, double *y, int32_t *status, i
 /* Per-problem exit data of the last QP solve: final merit (<= 1 when solved) and the number of
  * iterative-refinement steps taken (B entries each; NULL skips). */
 int cmpc_get_qp_info(cmpc_handle h, double *merit, int32_t *n_refine);
+/* Per problem, the Newton steps of the last QP solve that ran on the whole workgroup after the
+ * problem was handed over (grouped kernel k_qp_group: the last problem of a group, once the others
+ * have stopped); 0 for problems solved on their own waves only.  B entries. */
+int cmpc_get_qp_tail(cmpc_handle h, int32_t *tail_steps);
 /* The accepted iterate of each problem (X, U) with that iteration's LQR gains and covariances.
  * Reference mode serves K and Sigma from the live linearization arrays, which every iteration
  * recomputes bit-identically (quirk Q1; the reference keeps references to that iteration's

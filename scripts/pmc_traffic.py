@@ -7,34 +7,50 @@ both counters are in KB.  Usage: python scripts/pmc_traffic.py <fetch_dir> <writ
 import collections
 import csv
 import glob
+import hashlib
 import json
 import os
 import sys
 
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), '..')
 
-def per_kernel(d, counter):
+
+def per_kernel(d, counter, skip=0):
+    """{kernel: (sum of the counter, dispatches)} over each kernel's dispatches after its first
+    `skip` (the warm-up launches, in dispatch order)."""
     f = glob.glob(os.path.join(d, '**', '*counter_collection.csv'), recursive=True)[0]
-    tot, n = collections.defaultdict(float), collections.defaultdict(set)
+    per = collections.defaultdict(lambda: collections.defaultdict(float))
     for r in csv.DictReader(open(f)):
         if r['Counter_Name'] != counter:
             continue
         name = r['Kernel_Name'].split('(')[0]
-        tot[name] += float(r['Counter_Value'])
-        n[name].add(r['Dispatch_Id'])
-    return {k: (tot[k], len(n[k])) for k in tot}
+        per[name][int(r['Dispatch_Id'])] += float(r['Counter_Value'])
+    out = {}
+    for k, disp in per.items():
+        ids = sorted(disp)
+        ids = ids[skip:] if len(ids) > skip else ids
+        out[k] = (sum(disp[i] for i in ids), len(ids))
+    return out
 
 
 def main():
     fdir, wdir = sys.argv[1], sys.argv[2]
     out = sys.argv[3] if len(sys.argv) > 3 else os.path.join(os.path.dirname(__file__), '..', 'profiles',
                                                               'qp_pmc_traffic.json')
-    fe, wr = per_kernel(fdir, 'FETCH_SIZE'), per_kernel(wdir, 'WRITE_SIZE')
+    skip = int(os.environ.get('PMC_SKIP', '2'))   # warm-up launches of the profiled bench run
+    fe, wr = per_kernel(fdir, 'FETCH_SIZE', skip), per_kernel(wdir, 'WRITE_SIZE', skip)
     qp = sorted(k for k in fe if 'k_qp_ipm' in k or 'k_qp_group' in k)[0]   # the batch's QP kernel
     fkb, fn = fe[qp]
     wkb, wn = wr[qp]
     per_launch = (2.0 * fkb / fn + wkb / wn) * 1024.0
-    res = {'source': 'rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), python3 bench.py --steps 2 '
-                     '--warmup 0 --no-cpu-baseline',
+    lib = os.path.join(ROOT, 'centroidal-mpc_amd', 'cmpc', 'libcmpc.so')
+    res = {'source': 'rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes)',
+           'command': os.environ.get('PMC_BENCH_CMD', '?'),
+           'head': os.environ.get('CMPC_HEAD', '?'),
+           'lib_sha16': hashlib.sha256(open(lib, 'rb').read()).hexdigest()[:16] if os.path.exists(lib) else None,
+           'note': 'average over the QP dispatches of the run; with --warmup >= 2 the dispatches measured '
+                   'group problems by the previous launch\'s Newton counts (the timed steady state)',
+           'skipped_warmup_dispatches': skip,
            'kernel': qp, 'dispatches': {'FETCH_SIZE': fn, 'WRITE_SIZE': wn},
            'fetch_size_kb_per_launch': fkb / fn, 'write_size_kb_per_launch': wkb / wn,
            'correction': 'FETCH_SIZE x2 (MI355X_MICROARCH.md: gfx950 FETCH_SIZE reports half of the bytes of wide '

@@ -1,0 +1,122 @@
+"""GPU: the kernel that produces the headline number, checked against the oracle at the headline size.
+
+BASELINE.json's metric runs Solo12 trot, N=100, 1024 problems per GPU.  There the library launches the
+grouped QP kernel k_qp_group<4> (four problems per four-wave workgroup; the last problem of a group is
+handed over to all four waves, which finish it with the four-chain recurrence of schur_pt.hpp), and
+k_qp_order groups the problems by the Newton-step counts of the previous QP launch.  The bench times
+steps after warm-up launches, so the grouping it measures is the sorted one.  These tests reproduce
+exactly that: two fixed-K SCP iterations (the second one already sorted), then a third QP launch on the
+same batch with the same settings, whose QPs are compared with the oracle's independent sparse
+interior-point solver (oracle/sparse_ipm.py) on:
+  * the 8 problems with the most Newton steps, all of them finished on four waves (qp_tail > 0);
+  * 8 seeded random problems.
+Per problem: KKT residuals of the reference-form QP (the CSC the reference hands OSQP,
+src/scp_solver.py:59-68) -- primal <= 1e-8, dual <= 1e-6 x the cost scale, multiplier signs exact --
+and |X_gpu - X_oracle|_inf <= 1e-5 |X|_inf, the parity bar of tests/test_gpu_parity.py.
+The same on the 2-GPU shard of the metric (512 problems: k_qp_ipm<2>, two waves per problem) and the
+4-GPU shard (256 problems: k_qp_ipm<4>, four chains).
+"""
+import numpy as np
+import pytest
+
+from cmpc._lib import Solver
+from cmpc.synth import make_batch
+from oracle.kkt import kkt_residuals
+from oracle.sparse_ipm import solve_qp as sparse_ipm_qp
+
+pytestmark = pytest.mark.gpu
+
+N = 100
+
+
+def _sorted_launch(B, seed_offset):
+    pb = make_batch('trot', N, B, seed_offset=seed_offset)
+    s = Solver(pb.robot, N, B, 'fp64')
+    s.upload(pb)
+    kernel = s.qp_kernel()
+    s.scp_iterate(fixed_iters=True)
+    s.scp_iterate(fixed_iters=True)
+    # the third launch phase by phase, so the exported QP is exactly the one solved (scp_iterate's
+    # accept step would move the trust region after it)
+    s.linearize(); s.assemble(); s.qp_solve()
+    z, y, st, it = s.qp_solution(with_y=True)
+    return s, kernel, z, y, st, it
+
+
+def _check(s, z, y, b):
+    P, q, A, l, u = s.export_qp(b)
+    k = kkt_residuals(P, q, A, l, u, z[b], y[b])
+    scale = max(1.0, np.abs(P @ z[b]).max(), np.abs(q).max())
+    assert k['prim'] <= 1e-8, (b, k['prim'])
+    assert k['dual'] <= 1e-6 * scale, (b, k['dual'], scale)
+    assert k['sign'] == 0.0, b
+    ref = sparse_ipm_qp(P, q, A, l, u)
+    assert ref.info.status == 'solved'
+    nxu = 9 * (N + 1) + 12 * N
+    err = np.abs(z[b][:nxu] - ref.x[:nxu]).max() / np.abs(ref.x[:nxu]).max()
+    assert err <= 1e-5, (b, err)
+
+
+def _sample(it, n_slow=8, n_rand=8, seed=0):
+    slow = [int(b) for b in np.argsort(-it, kind='stable')[:n_slow]]
+    rng = np.random.default_rng(seed)
+    rest = np.setdiff1d(np.arange(len(it)), slow)
+    return slow, [int(b) for b in rng.choice(rest, n_rand, replace=False)]
+
+
+def test_metric_config_kernel_matches_oracle():
+    B = 1024
+    s, kernel, z, y, st, it = _sorted_launch(B, seed_offset=0)
+    tail = s.qp_tail()
+    merit, _ = s.qp_info()
+    try:
+        assert kernel == 'k_qp_group<4>', kernel
+        assert np.all(st == 1), np.unique(st, return_counts=True)
+        assert np.all(merit <= 1.0)
+        slow, rand = _sample(it)
+        # the slowest problems are the ones the group hands over to four waves
+        assert all(tail[b] > 0 for b in slow), [(b, int(it[b]), int(tail[b])) for b in slow]
+        for b in slow + rand:
+            _check(s, z, y, b)
+    finally:
+        s.close()
+
+
+@pytest.mark.parametrize('B,kernel', [(512, 'k_qp_ipm<2>'), (256, 'k_qp_ipm<4>')])
+def test_metric_shards_match_oracle(B, kernel):
+    """The 2- and 4-GPU slices of the metric's 1024 problems (cmpc/shard.py: contiguous slices)."""
+    s, k, z, y, st, it = _sorted_launch(B, seed_offset=0)
+    try:
+        assert k == kernel, k
+        assert np.all(st == 1), np.unique(st, return_counts=True)
+        slow, rand = _sample(it, n_slow=4, n_rand=4, seed=1)
+        for b in slow + rand:
+            _check(s, z, y, b)
+    finally:
+        s.close()
+
+
+def test_metric_config_first_launch_of_a_fresh_batch():
+    """A never-solved batch (the reference's use: every solve_scp call is a new problem,
+    src/scp_solver.py:118-179): its first grouped launch has no Newton counts to sort by.  All
+    problems solved, and a handle that solved another batch before gives bit-identical results (no
+    ordering key leaks from the previous upload)."""
+    B = 1024
+    pa = make_batch('trot', N, B, seed_offset=0)
+    pb = make_batch('trot', N, B, seed_offset=5000)
+    s = Solver(pa.robot, N, B, 'fp64')
+    s.upload(pa)
+    s.scp_iterate(fixed_iters=True)
+    s.scp_iterate(fixed_iters=True)
+    s.upload(pb)
+    s.scp_iterate(fixed_iters=True)
+    z1, _, st1, it1 = s.qp_solution(with_y=False)
+    s.close()
+    s2 = Solver(pb.robot, N, B, 'fp64')
+    s2.upload(pb)
+    s2.scp_iterate(fixed_iters=True)
+    z2, _, st2, it2 = s2.qp_solution(with_y=False)
+    s2.close()
+    assert np.all(st1 == 1)
+    np.testing.assert_array_equal(it1, it2)
+    np.testing.assert_array_equal(z1, z2)

@@ -14,12 +14,21 @@ from cmpc.synth import make_batch
 
 
 def test_shard_bounds_tile_the_batch():
-    for B in (1, 2, 7, 1024, 1025):
-        for world in (1, 2, 3, 8):
+    """Contiguous slices of floor / ceil(B / world): none empty while B >= world (an empty rank could
+    not take part in the gather), equal at the metric's 1024 over 1/2/4/8 ranks."""
+    for B in (1, 2, 7, 9, 1024, 1025):
+        for world in (1, 2, 3, 4, 8):
+            if B < world:
+                with pytest.raises(ValueError):
+                    shard_bounds(B, 0, world)
+                continue
             spans = [shard_bounds(B, r, world) for r in range(world)]
             assert spans[0][0] == 0 and spans[-1][1] == B
             assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
-            assert all(hi - lo <= -(-B // world) for lo, hi in spans)
+            sizes = [hi - lo for lo, hi in spans]
+            assert min(sizes) >= 1 and max(sizes) - min(sizes) <= 1
+    assert [shard_bounds(1024, r, 8) for r in range(8)] == [(128 * r, 128 * (r + 1)) for r in range(8)]
+    assert [shard_bounds(9, r, 4)[1] - shard_bounds(9, r, 4)[0] for r in range(4)] == [2, 2, 2, 3]
     with pytest.raises(ValueError):
         shard_bounds(4, 2, 2)
 
