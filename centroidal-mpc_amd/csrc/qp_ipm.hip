@@ -25,10 +25,15 @@
 #include "common.hpp"
 #include "cov_scan.hpp"
 
+// Phases are always inlined: an outlined phase gets its Ctx by reference, i.e. a generic pointer to
+// the caller's scratch, and then does every access through flat instructions (round 4: the
+// refinement phases phase_lres / phase_dz_refine were outlined in k_qp_group<.., 2> once the kernel
+// grew, 431 flat loads and stores, and the kernel faulted with a memory aperture violation on its
+// first refinement; inlined, no flat instruction is left).  CMPC_NOINLINE (diagnostic builds) outlines them.
 #ifdef CMPC_NOINLINE
 #define PHASE_ATTR __attribute__((noinline))
 #else
-#define PHASE_ATTR
+#define PHASE_ATTR __attribute__((always_inline))
 #endif
 #define WF(f) (Ws<ROBOT>::f)   // workspace field row
 #ifndef QP_MIN_WAVES
@@ -60,7 +65,7 @@ template <int ROBOT> struct Ws {
         s = 0, l = s + NI, x = l + NI, u = x + 9, t = u + NU, nu = t + 1, rdx = nu + 9, rdt = rdx + 9,
         rdu = rdt + 1, rde = rdu + NU, rdi = rde + 9, facx = rdi + NI, facu = facx + FX, wx = facu + NC * FU,
         wt = wx + 9, wu = wt + 1, dx = wu + NU, dt = dx + 9, du = dt + 1, ds = du + NU, dl = ds + NI,
-        dsa = dl + NI, dla = dsa + NI, rh = dla + NI, dn0 = rh + NI, NF = dn0 + 9
+        dsa = dl + NI, dla = dsa + NI, dn0 = dla + NI, NF = dn0 + 9
     };
     // Schur blocks (block-major 9x9): S_jj -> I_j, and S_{j,j+1} -> X_{j+1} / Y_j (tw_factor_ends);
     // four-wave workgroups also the fill factors H_j and the separator scratch (schur_pt.hpp)
@@ -145,6 +150,15 @@ template <typename T, int ROBOT, typename SR> __device__ __forceinline__ void op
     }
 }
 
+// The three separator blocks of the four-chain recurrence (schur_pt.hpp).  Passed by value to the
+// outlined chain functions: as a reference to an array in the caller's scratch every access was a
+// flat load.
+struct Seps {
+    int v[3];
+    __device__ __forceinline__ int operator[](int i) const { return v[i]; }
+    __device__ __forceinline__ int &operator[](int i) { return v[i]; }
+};
+
 // ------------------------------------------------------------------ per-problem context
 template <typename T, int ROBOT> struct Ctx {
     static constexpr int NC = Robot<ROBOT>::NC, NUPC = Robot<ROBOT>::NUPC, FO = Robot<ROBOT>::FO;
@@ -181,7 +195,7 @@ template <typename T, int ROBOT> struct Ctx {
     LdsT<T> *wxs = nullptr;
     LdsT<T> *bus = nullptr;   // four-wave split w phases: B w_u of knot k at block 1 + k (add_wx)
     T *Sh = nullptr, *Sx = nullptr;   // four-wave workgroups: fill factors, separator scratch (schur_pt.hpp)
-    int sp[3] = {0, 0, 0};            // four-wave workgroups: separator blocks
+    Seps sp{{0, 0, 0}};               // four-wave workgroups: separator blocks
     LdsT<T> *sbv = nullptr, *hy = nullptr;   // separator right-hand-side terms, fill products
     __device__ unsigned cmask(int k) const { return cm ? unsigned(cm[k]) : cmask_mem(k); }
     __device__ unsigned cmask_mem(int k) const {
@@ -695,8 +709,10 @@ __device__ __forceinline__ void phase_factor(const Ctx<T, ROBOT> &C, int k, cons
     for (int c = 0; c < (PART != 0 ? NC : 0); ++c) {
         const SV<T> fu = C.kv(WF(facu), k) + c * FU;
         const bool act = (msk >> c) & 1u;
-        // Winvd: inverse diagonal of W' (CoP rows fold into their coordinate's diagonal)
-        for (int q = 0; q < NUPC; ++q) fu[FU_WI + q] = C.iWu(NUPC * c + q);
+        // Winvd: inverse diagonal of W' (CoP rows fold into their coordinate's diagonal); TALOS only:
+        // Solo12's is 1 / Wu, which phase_sblock does not need (no CoP columns)
+        if (ROBOT == 1)
+            for (int q = 0; q < NUPC; ++q) fu[FU_WI + q] = C.iWu(NUPC * c + q);
         if (ROBOT == 1 && act) {
             for (int dd = 0; dd < 2; ++dd) {
                 const int r0 = R_::CP + 4 * c + 2 * dd;
@@ -779,7 +795,7 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_sblock(const C
         ldv(cs + S::LEVER, lev[c]);
         const SV<T> fu = C.kv(WF(facu), k) + c * FU;
         ldv(fu + FU_F, F[c]);
-        ldv(fu + FU_WI, wd[c]);
+        if (ROBOT == 1) ldv(fu + FU_WI, wd[c]);
     }
     T bc[NC][6], bt[NC][3];
     if (ROBOT == 1)
@@ -1429,36 +1445,37 @@ __device__ void tw_solve_back(const T *Xs, int NB, int m, LdsT<T> *vb, LdsT<T> *
 
 #include "schur_pt.hpp"
 
-// r_hat = r_i - r_c / lambda for the rows of knot k.  corr 0 (predictor): r_c = s lambda; 1
-// (corrector): r_c = s lambda + ds_aff dlambda_aff - sigma mu; 2 (refinement): r_c = the dsa
-// field, which then holds the complementarity residual of the corrector direction (phase_lres)
-// rows [R0, R1): all of them, or one part's (PART as in resid_knot)
+// r_hat = r_i - r_c / lambda of one row.  corr 0 (predictor): r_c = s lambda; 1 (corrector):
+// r_c = s lambda + ds_aff dlambda_aff - sigma mu (a = the dsa field: the predictor's product);
+// 2 (refinement): r_c = a, the dsa field then holding the complementarity residual of the corrector
+// direction (phase_lres).  Absent rows: 0.  The w phase and the direction phase both form it (the
+// direction phase recomputes it from s, lambda, r_i and dsa, which it loads anyway, instead of a
+// stored r_hat: one field row less written and read per Newton solve).
+template <typename T>
+__device__ __forceinline__ T rhat_row(int corr, bool pr, T rd, T sr, T lr, T a, T sigma_mu) {
+    const T cc = corr ? (corr == 2 ? a : a - sigma_mu) : T(0);
+    const T rc = (corr == 2 ? T(0) : sr * lr) + cc;
+    const T v = rd - fdiv(rc, pr ? lr : T(1));
+    return pr ? v : T(0);
+}
+// r_hat for the rows of knot k, rows [R0, R1): all of them, or one part's (PART as in resid_knot)
 template <typename T, int ROBOT, int R0 = 0, int R1 = Rows<ROBOT>::NI>
 __device__ __forceinline__ void rhat_rows(const Ctx<T, ROBOT> &C, int k, int corr, T sigma_mu, const T *s, const T *lm,
                                           T *rh) {
     constexpr int NI = Rows<ROBOT>::NI;
     const unsigned msk = C.cmask(k);
     // every row's loads in one batch (a branch per row serialized them)
-    T rd[NI], cc[NI];
+    T rd[NI], a[NI];
     const SV<T> rdi = C.kv(WF(rdi), k);
 #pragma unroll
-    for (int r = R0; r < R1; ++r) { rd[r] = rdi[r]; cc[r] = T(0); }
+    for (int r = R0; r < R1; ++r) { rd[r] = rdi[r]; a[r] = T(0); }
     if (corr) {   // corrector: + ds_aff dlambda_aff - sigma mu (the product, stored by the predictor)
-        T a[NI];
         const SV<T> dsa = C.kv(WF(dsa), k);
 #pragma unroll
         for (int r = R0; r < R1; ++r) a[r] = dsa[r];
-#pragma unroll
-        for (int r = R0; r < R1; ++r) cc[r] = corr == 2 ? a[r] : a[r] - sigma_mu;
     }
 #pragma unroll
-    for (int r = R0; r < R1; ++r) {
-        const bool pr = Ctx<T, ROBOT>::present_m(msk, r);
-        const T sr = s[r], lr = lm[r];
-        const T rc = (corr == 2 ? T(0) : sr * lr) + cc[r];
-        const T v = rd[r] - fdiv(rc, pr ? lr : T(1));
-        rh[r] = pr ? v : T(0);
-    }
+    for (int r = R0; r < R1; ++r) rh[r] = rhat_row(corr, Ctx<T, ROBOT>::present_m(msk, r), rd[r], s[r], lm[r], a[r], sigma_mu);
 }
 
 // (5a) particular solution w = Phi^-1 (r_d + G' D rhat) (friction rows in push-through form)
@@ -1476,7 +1493,7 @@ __device__ __forceinline__ void phase_w_core(const Ctx<T, ROBOT> &C, int k, int 
     const bool hu = k < N;
     constexpr int RA = PART == 1 ? R_::FR : 0, RB = PART == 0 ? R_::FR : NI;   // this part's rows
     T rh[NI];
-    rhat_rows<T, ROBOT, RA, RB>(C, k, corr, sigma_mu, sv, lv, rh);   // kept for phase_dz (stored below)
+    rhat_rows<T, ROBOT, RA, RB>(C, k, corr, sigma_mu, sv, lv, rh);   // (phase_dz forms it again)
     T rdx[9], rdu[NU];
     ldv(C.kv(WF(rdx), k), rdx);
     ldv(C.kv(WF(rdu), k), rdu);   // k = N: unused
@@ -1534,11 +1551,6 @@ __device__ __forceinline__ void phase_w_core(const Ctx<T, ROBOT> &C, int k, int 
     // stores
     (void)wt;   // w_x, w_t enter only the right-hand side below; w_u is read by phase_dz
     if (hu && PART != 0) stv(C.kv(WF(wu), k), ou);
-    {
-        const SV<T> rhs = C.kv(WF(rh), k);
-#pragma unroll
-        for (int r = RA; r < RB; ++r) rhs[r] = rh[r];
-    }
     // the Schur right-hand side, fused: block 1 + k = r_k - A_k wx_k - B_k wu_k + wx_{k+1}.  Thread
     // k writes all but the last term; after a wave-level fence (block k was written by lane k - 1
     // in this pass or an earlier one: the lanes of the one wave run in lockstep) it adds its own
@@ -1618,9 +1630,14 @@ __device__ __forceinline__ void phase_w_pred(const Ctx<T, ROBOT> &C, int k, cons
 // direction becomes direction + correction and the ratio test runs on the sum.
 // PART as in resid_knot: 0 the (x, t) part and the trust-region / slack rows, 1 the controls and
 // the contact rows (-1 both)
+// r_hat is formed here again (rhat_row with corr / sigma_mu, from s, lambda, r_i and, corr >= 1,
+// the dsa field), as the w phase formed it.  prod (the predictor after the initialization step):
+// only ds_aff dlambda_aff is stored; its dx, dt, du and dlambda are dead (the corrector replaces
+// them), so they are not written.
 template <typename T, int ROBOT, bool ACC = false, int PART = -1>
-__device__ __forceinline__ T dz_knot(const Ctx<T, ROBOT> &C, int k, T (&mus)[3], bool prod, const T *__restrict__ stp,
-                                     const T *__restrict__ rhp, const T *__restrict__ rdxp, const T *__restrict__ rdtp,
+__device__ __forceinline__ T dz_knot(const Ctx<T, ROBOT> &C, int k, T (&mus)[3], bool prod, int corr, T sigma_mu,
+                                     const T *__restrict__ stp,
+                                     const T *__restrict__ dsap, const T *__restrict__ rdxp, const T *__restrict__ rdtp,
                                      const T *__restrict__ wup, const T *__restrict__ ss, const T *__restrict__ ls,
                                      const T *__restrict__ rdip, const T *__restrict__ rdup,
                                      T *__restrict__ dxo, T *__restrict__ dto, T *__restrict__ duo, T *__restrict__ ds,
@@ -1652,7 +1669,7 @@ __device__ __forceinline__ T dz_knot(const Ctx<T, ROBOT> &C, int k, T (&mus)[3],
         T dsr = pr ? -rdir - g : T(0);
         if (ACC) { dsr += ds[r * ld]; dlr += dl[r * ld]; }
         ds[r * ld] = prod ? dsr * dlr : dsr;
-        dl[r * ld] = dlr;
+        if (!prod) dl[r * ld] = dlr;
         // sum_r (s + a ds)(lambda + a dl) = mus0 + a mus1 + a^2 mus2 (absent rows: lambda = ds = dl = 0)
         mus[0] = fma(sr, lr, mus[0]);
         mus[1] = fma(sr, dlr, fma(lr, dsr, mus[1]));
@@ -1668,15 +1685,20 @@ __device__ __forceinline__ T dz_knot(const Ctx<T, ROBOT> &C, int k, T (&mus)[3],
     for (int q = 0; q < (PART != 0 ? NU : 0); ++q) { wuv[q] = wup[q * ld]; rduv[q] = rdup[q * ld]; }
     // (x, t) part and the trust-region / slack rows
     if (PART != 1) {
-        T rdx[9], s9[9], l9[9], rh9[9], ri9[9];
+        T rdx[9], s9[9], l9[9], rh9[9], ri9[9], a9[9];
 #pragma unroll
         for (int i = 0; i < 9; ++i) {
             rdx[i] = rdxp[i * ld];
             s9[i] = ss[i * ld];
             l9[i] = ls[i * ld];
-            rh9[i] = rhp[i * ld];
             ri9[i] = rdip[i * ld];
+            a9[i] = T(0);
         }
+        if (corr)
+#pragma unroll
+            for (int i = 0; i < 9; ++i) a9[i] = dsap[i * ld];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) rh9[i] = rhat_row(corr, true, ri9[i], s9[i], l9[i], a9[i], sigma_mu);
         const T rdt = rdtp[0];
         T dx[9], dtt, dlt[8], dls;
         for (int i = 0; i < 6; ++i) dx[i] = -C.iWx(i) * (rdx[i] + ex[i]);
@@ -1687,9 +1709,11 @@ __device__ __forceinline__ T dz_knot(const Ctx<T, ROBOT> &C, int k, T (&mus)[3],
             tr_local(C, Lk, z1, dsl, iden, vL, -rdt, rh9, dx + 6, dtt, dlt, dls);
         }
         // the rows' g'dz use the correction itself (ds = -r_i - g'dz is linear in the solve)
+        if (!prod) {
 #pragma unroll
-        for (int i = 0; i < 9; ++i) dxo[i * ld] = ACC ? dxo[i * ld] + dx[i] : dx[i];
-        dto[0] = ACC ? dto[0] + dtt : dtt;
+            for (int i = 0; i < 9; ++i) dxo[i * ld] = ACC ? dxo[i * ld] + dx[i] : dx[i];
+            dto[0] = ACC ? dto[0] + dtt : dtt;
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j)
             emit(j, true, tr_sign<T>(j, 0) * dx[6] + tr_sign<T>(j, 1) * dx[7] + tr_sign<T>(j, 2) * dx[8] + C.cw * dtt,
@@ -1701,12 +1725,15 @@ __device__ __forceinline__ T dz_knot(const Ctx<T, ROBOT> &C, int k, T (&mus)[3],
     for (int c = 0; c < (PART != 0 ? NC : 0); ++c) {
         const bool pr = hu && ((msk >> c) & 1u);
         const auto cs = st + (S::CON + S::CS * c);
-        T G[12], s4[4], l4[4], rh4[4], ri4[4], vf[3];
+        T G[12], s4[4], l4[4], rh4[4], ri4[4], a4[4] = {T(0), T(0), T(0), T(0)}, vf[3];
         for (int e = 0; e < 12; ++e) G[e] = cs[S::G + e];
         for (int r = 0; r < 4; ++r) {
             const int row = R_::FR + 4 * c + r;
-            s4[r] = ss[row * ld]; l4[r] = ls[row * ld]; rh4[r] = rhp[row * ld]; ri4[r] = rdip[row * ld];
+            s4[r] = ss[row * ld]; l4[r] = ls[row * ld]; ri4[r] = rdip[row * ld];
         }
+        if (corr)
+            for (int r = 0; r < 4; ++r) a4[r] = dsap[(R_::FR + 4 * c + r) * ld];
+        for (int r = 0; r < 4; ++r) rh4[r] = rhat_row(corr, pr, ri4[r], s4[r], l4[r], a4[r], sigma_mu);
         const T wi[3] = {C.iWu(NUPC * c + FO), C.iWu(NUPC * c + FO + 1), C.iWu(NUPC * c + FO + 2)};
         T Gw[4][3], Ki[10], F[6], wd[NUPC], au[NUPC], du[NUPC];
         fric_factor(G, wi, s4, l4, pr, Gw, Ki);
@@ -1723,7 +1750,7 @@ __device__ __forceinline__ T dz_knot(const Ctx<T, ROBOT> &C, int k, T (&mus)[3],
         // select on a loaded value becomes a branch around the load and a wait per row
         const T hf = hu ? T(1) : T(0);
         for (int q = 0; q < NUPC; ++q) du[q] = (-wuv[NUPC * c + q] - au[q]) * hf;
-        if (hu)
+        if (hu && !prod)
             for (int q = 0; q < NUPC; ++q) duo[(NUPC * c + q) * ld] = ACC ? duo[(NUPC * c + q) * ld] + du[q] : du[q];
         for (int i = 0; i < 3; ++i) vf[i] = -(rduv[NUPC * c + FO + i] + ec[FO + i]) * hf;
         T z[4];
@@ -1739,9 +1766,10 @@ __device__ __forceinline__ T dz_knot(const Ctx<T, ROBOT> &C, int k, T (&mus)[3],
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int r = R_::CP + 4 * c + q, dd = q / 2;
-                const T sr = ss[r * ld], lr = ls[r * ld];
+                const T sr = ss[r * ld], lr = ls[r * ld], rir = rdip[r * ld], ar = corr ? dsap[r * ld] : T(0);
                 const T gr = (q % 2 == 0) ? du[dd] : -du[dd];
-                emit(r, pr, gr, pr ? C.Dform(lr, sr) * (gr + rhp[r * ld]) : T(0), sr, lr, rdip[r * ld]);
+                const T rhr = rhat_row(corr, pr, rir, sr, lr, ar, sigma_mu);
+                emit(r, pr, gr, pr ? C.Dform(lr, sr) * (gr + rhr) : T(0), sr, lr, rir);
             }
         }
     }
@@ -1749,10 +1777,11 @@ __device__ __forceinline__ T dz_knot(const Ctx<T, ROBOT> &C, int k, T (&mus)[3],
 }
 
 template <typename T, int ROBOT, int PART = -1>
-__device__ PHASE_ATTR T phase_dz(const Ctx<T, ROBOT> &C, int k, int corr, bool init, T (&mus)[3]) {
+__device__ PHASE_ATTR T phase_dz(const Ctx<T, ROBOT> &C, int k, int corr, bool init, T sigma_mu, T (&mus)[3]) {
     const int kc = k < C.N ? k : 0;   // k = N: no controls or contacts
     T *ws = C.ws;
-    return dz_knot<T, ROBOT, false, PART>(C, k, mus, !corr && !init, C.stage + kc, ws + WF(rh) * KPC + k, ws + WF(rdx) * KPC + k,
+    return dz_knot<T, ROBOT, false, PART>(C, k, mus, !corr && !init, corr, sigma_mu, C.stage + kc,
+                             ws + WF(dsa) * KPC + k, ws + WF(rdx) * KPC + k,
                              ws + WF(rdt) * KPC + k, ws + WF(wu) * KPC + kc, ws + WF(s) * KPC + k,
                              ws + WF(l) * KPC + k, ws + WF(rdi) * KPC + k, ws + WF(rdu) * KPC + kc,
                              ws + WF(dx) * KPC + k, ws + WF(dt) * KPC + k,
@@ -1766,7 +1795,7 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR T phase_dz_refine(const C
     const int kc = k < C.N ? k : 0;
     T *ws = C.ws;
     T mus[3] = {T(0), T(0), T(0)};
-    return dz_knot<T, ROBOT, true>(C, k, mus, false, C.stage + kc, ws + WF(rh) * KPC + k, ws + WF(rdx) * KPC + k,
+    return dz_knot<T, ROBOT, true>(C, k, mus, false, 2, T(0), C.stage + kc, ws + WF(dsa) * KPC + k, ws + WF(rdx) * KPC + k,
                                    ws + WF(rdt) * KPC + k, ws + WF(wu) * KPC + kc, ws + WF(s) * KPC + k,
                                    ws + WF(l) * KPC + k, ws + WF(rdi) * KPC + k, ws + WF(rdu) * KPC + kc,
                                    ws + WF(dx) * KPC + k, ws + WF(dt) * KPC + k, ws + WF(du) * KPC + k,
@@ -2377,12 +2406,12 @@ __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT>
             T am[1] = {T(1)}, mus[3] = {T(0), T(0), T(0)};
             if constexpr (split_knots<G>()) {
                 if (__builtin_amdgcn_readfirstlane(tid) < 128) {
-                    for (int k = tid & 127; k < K1; k += 128) am[0] = fmin(am[0], phase_dz<T, ROBOT, 0>(C, k, corr, init, mus));
+                    for (int k = tid & 127; k < K1; k += 128) am[0] = fmin(am[0], phase_dz<T, ROBOT, 0>(C, k, corr, init, sigma_mu, mus));
                 } else {
-                    for (int k = tid & 127; k < K1; k += 128) am[0] = fmin(am[0], phase_dz<T, ROBOT, 1>(C, k, corr, init, mus));
+                    for (int k = tid & 127; k < K1; k += 128) am[0] = fmin(am[0], phase_dz<T, ROBOT, 1>(C, k, corr, init, sigma_mu, mus));
                 }
             } else {
-                for (int k = tid; k < K1; k += G) am[0] = fmin(am[0], phase_dz<T, ROBOT>(C, k, corr, init, mus));
+                for (int k = tid; k < K1; k += G) am[0] = fmin(am[0], phase_dz<T, ROBOT>(C, k, corr, init, sigma_mu, mus));
             }
             block_reduce<T, G, 1, 2, WG>(am, L.red);
             STAMP(7);

@@ -37,7 +37,7 @@ constexpr int PT_SCRATCH = TW_SCRATCH + 2 * 88;
 // trot N=100 x 128 with the fp64 matrix-core fill, 5.4k against 4.0k cycles; fp32, VALU fill,
 // ~1.6x), so the ends get the larger share of the non-separator blocks: le = r li with
 // 2 le + 2 li = NB - 3, r = 1.35 (fp64) / 1.6 (fp32).
-template <typename T> __device__ __forceinline__ void pt_seps(int NB, int (&s)[3]) {
+template <typename T> __device__ __forceinline__ void pt_seps(int NB, Seps &s) {
     const int le = sizeof(T) == 8 ? (NB - 3) * 135 / 470 : (NB - 3) * 8 / 26, rem = NB - 3 - 2 * le, li = rem / 2;
     s[0] = le;
     s[1] = s[0] + 1 + li;
@@ -82,7 +82,7 @@ __device__ __forceinline__ void pt_contrib(const LdsT<T> *Op, const LdsT<T> *P, 
 // One chain per wave (see the file comment), the predictor's forward elimination fused in (vb).
 // sbv: separator right-hand-side terms, [c][0] from above, [c][1] from below (9 each).
 template <typename T>
-__device__ __attribute__((noinline)) void pt_factor_chains(T *Sd_, T *So_, T *Sh_, T *Sx_, int NB, const int (&sp)[3], LdsT<T> *shw, LdsT<T> *vb,
+__device__ __attribute__((noinline)) void pt_factor_chains(T *Sd_, T *So_, T *Sh_, T *Sx_, int NB, Seps sp, LdsT<T> *shw, LdsT<T> *vb,
                                  LdsT<T> *sbv) {
     GlbT<T> *Sd = (GlbT<T> *)Sd_, *So = (GlbT<T> *)So_, *Sh = (GlbT<T> *)Sh_, *Sx = (GlbT<T> *)Sx_;
     constexpr int L = 64, NE = 2;
@@ -284,7 +284,7 @@ __device__ __attribute__((noinline)) void pt_factor_chains(T *Sd_, T *So_, T *Sh
 // factors (corrector / refinement).  The right-hand side of separator c is b_{s_c} minus its terms
 // from above and below (sbv; the interior chains' fill terms for the solves come from hy).
 template <typename T>
-__device__ __attribute__((noinline)) void pt_reduced(T *Sd_, T *Sx_, const int (&sp)[3], LdsT<T> *shw, LdsT<T> *vb, const LdsT<T> *sbv, bool factor) {
+__device__ __attribute__((noinline)) void pt_reduced(T *Sd_, T *Sx_, Seps sp, LdsT<T> *shw, LdsT<T> *vb, const LdsT<T> *sbv, bool factor) {
     GlbT<T> *Sd = (GlbT<T> *)Sd_, *Sx = (GlbT<T> *)Sx_;
     const int l = threadIdx.x & 63;
     LdsT<T> *A = shw, *P = A + 88, *Xb = A + 176, *Ob = A + 264, *Dd = A + 352, *Dn = A + 368;
@@ -347,7 +347,7 @@ __device__ __attribute__((noinline)) void pt_reduced(T *Sd_, T *Sx_, const int (
 
 // Forward elimination of a right-hand side (vb) along the four chains (lanes 0..31 of each wave,
 // one block ring per wave); the separators' X / Y terms into sbv[c][0] / sbv[2][1].
-template <typename T> __device__ __attribute__((noinline)) void pt_solve_elim(const T *Xs, int NB, const int (&sp)[3], LdsT<T> *vb, LdsT<T> *ring, LdsT<T> *sbv) {
+template <typename T> __device__ __attribute__((noinline)) void pt_solve_elim(const T *Xs, int NB, Seps sp, LdsT<T> *vb, LdsT<T> *ring, LdsT<T> *sbv) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     if (l >= 32) return;
     const bool bottom = w == 3;
@@ -384,7 +384,7 @@ template <typename T> __device__ __attribute__((noinline)) void pt_solve_elim(co
 
 // fill terms of the interior chunks' left separators: hy[t] = (H_j y_j)_i for block j of chunk
 // 1 or 2, row i (all threads), summed per separator into sbv[c][1] by wave 0 after a barrier
-template <typename T, int NTT> __device__ __attribute__((noinline)) void pt_fill_rhs(const T *Sh_, const int (&sp)[3], const LdsT<T> *vb, LdsT<T> *hy) {
+template <typename T, int NTT> __device__ __attribute__((noinline)) void pt_fill_rhs(const T *Sh_, Seps sp, const LdsT<T> *vb, LdsT<T> *hy) {
     const GlbT<T> *Sh = (const GlbT<T> *)Sh_;
     const int a = sp[0] + 1, n = sp[2] - a;   // blocks s0+1 .. s2-1 (the separator s1 between them gives 0)
     for (int t = threadIdx.x; t < 9 * n; t += NTT) {
@@ -398,7 +398,7 @@ template <typename T, int NTT> __device__ __attribute__((noinline)) void pt_fill
         hy[t] = s;
     }
 }
-template <typename T> __device__ void pt_fill_sum(const int (&sp)[3], const LdsT<T> *hy, LdsT<T> *sbv) {
+template <typename T> __device__ void pt_fill_sum(Seps sp, const LdsT<T> *hy, LdsT<T> *sbv) {
     const int l = threadIdx.x & 63;
     if (l < 18) {
         const int c = l / 9, i = l % 9, a = sp[0] + 1;
@@ -412,7 +412,7 @@ template <typename T> __device__ void pt_fill_sum(const int (&sp)[3], const LdsT
 
 // local back-substitution terms of every non-separator block (all threads):
 // z_j = I_j y_j (- H_j' x_L for the interior chunks' blocks)
-template <typename T, int NTT> __device__ __attribute__((noinline)) void pt_solve_local(const T *Ii, const T *Sh_, int NB, const int (&sp)[3], LdsT<T> *vb) {
+template <typename T, int NTT> __device__ __attribute__((noinline)) void pt_solve_local(const T *Ii, const T *Sh_, int NB, Seps sp, LdsT<T> *vb) {
     const GlbT<T> *Sh = (const GlbT<T> *)Sh_;
     for (int j = threadIdx.x; j < NB; j += NTT) {
         if (j == sp[0] || j == sp[1] || j == sp[2]) continue;
@@ -452,7 +452,7 @@ template <typename T, int NTT> __device__ __attribute__((noinline)) void pt_solv
 // back substitution along the chains (lanes 0..31 of each wave): top-down chunks from their last
 // block up, x_j = z_j - X_{j+1}' x_{j+1} (X_{j+1} at So[j]); the bottom chunk down from s2 + 1,
 // x_j = z_j - Y_{j-1}' x_{j-1} (Y_{j-1} at So[j-1])
-template <typename T> __device__ __attribute__((noinline)) void pt_solve_back(const T *Xs, int NB, const int (&sp)[3], LdsT<T> *vb, LdsT<T> *ring) {
+template <typename T> __device__ __attribute__((noinline)) void pt_solve_back(const T *Xs, int NB, Seps sp, LdsT<T> *vb, LdsT<T> *ring) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     if (l >= 32) return;
     const bool bottom = w == 3;

@@ -75,6 +75,14 @@ def _chol_floor(S, floor):
     return L
 
 
+def max_step(v, dv, mk):
+    """Largest step in (0, 1] keeping v + a dv >= 0 on the rows of mask mk."""
+    neg = (dv < 0) & (mk > 0)
+    if not np.any(neg):
+        return 1.0
+    return min(1.0, float(np.min(-v[neg] / dv[neg])))
+
+
 def _fslot(qp):
     return 0 if qp.robot == 'solo12' else 2
 
@@ -85,7 +93,9 @@ INIT_FLOOR_L = 0.1        # lambda floor
 
 def solve(qp, eps=1e-11, max_iter=60, eta=0.999, verbose=False, reg=0.0, piv_floor=1e-13, dcap_rel=1e12,
           refine_alpha=0.5, refine_merit=1e6, eps_pinf=1e-4, init_floor=INIT_FLOOR,
-          init_floor_l=INIT_FLOOR_L, fric_floor=1e-9):
+          init_floor_l=INIT_FLOOR_L, fric_floor=1e-9, polish=False, polish_eps=None, polish_rel=1e-14):
+    if polish_eps is None:
+        polish_eps = eps
     N, nc, nu, nupc = qp.N, qp.nc, qp.nu, qp.nupc
     fo = _fslot(qp)
     talos = qp.robot != 'solo12'
@@ -157,6 +167,8 @@ def solve(qp, eps=1e-11, max_iter=60, eta=0.999, verbose=False, reg=0.0, piv_flo
     s = [mk * 1.0 + (1 - mk) for mk in masks]
     lam = [mk * 1.0 for mk in masks]
     stall = 0; mu_prev = None
+    polished_try = False; polish_log = []; last = None
+    system_at = lambda *a_: system(*a_)   # (bound below, once per iteration)
     n_refine = 0; merit = np.inf; prim_prev = 0.0
     hs = [qp.btr, np.zeros(N + 1), qp.fh]
     if talos:
@@ -195,6 +207,17 @@ def solve(qp, eps=1e-11, max_iter=60, eta=0.999, verbose=False, reg=0.0, piv_flo
         if not init and merit <= 1.0:
             status = 1
             break
+        # solution polishing once the iterate meets eps_polish (looser than eps): accepted -> done;
+        # rejected -> the interior-point iterations go on to eps
+        if polish and not polished_try and not init and it > 1 and merit * eps / polish_eps <= 1.0:
+            polished_try = True
+            pol = _polish(qp, masks, x, u, t, nu_, s, lam, last, system_at, GT, ET, Ez, ineq_val, e_rhs,
+                          polish_eps, talos, polish_rel)
+            polish_log.append(pol)
+            if pol['status'] == 1:
+                x, u, t, nu_, lam, s = pol['x'], pol['u'], pol['t'], pol['nu'], pol['lam'], pol['s']
+                status = 1
+                break
         # primal infeasibility (Farkas): E'nu + G'lambda -> 0 relative to |(nu, lambda)| while
         # b'nu + h'lambda < 0 (OSQP's test, on the multipliers, which diverge along the certificate)
         # (evaluated, as in the kernel, once the primal residual stagnates away from the solution)
@@ -214,165 +237,163 @@ def solve(qp, eps=1e-11, max_iter=60, eta=0.999, verbose=False, reg=0.0, piv_flo
             status = 2
             break
         # ---- factorization ----
-        D = [li / si * mk for li, si, mk in zip(lam, s, masks)]
-        # cap D on the rows handled in D-form (TR, slack, CoP): beyond ~1e12 x the stage
-        # curvature the products D * r lose all precision; the capped Newton step is an inexact
-        # Newton step on exact residuals (convergence is driven by the residuals)
-        dcap = dcap_rel * max(float(np.max(qp.Wx)), 1.0)
-        if talos:
-            D[3] = np.minimum(D[3], dcap)
-        # x/t block: Phi_LL, Phi_Lt, Phi_tt
-        # (L, t) block in push-through form.  Unknowns dL (3), dt, dlam_TR (8), dlam_sl:
-        #   W dL + G' dlam = vL ;  cw 1'dlam - dlam_sl = vt ;  G dL + cw 1 dt - D^-1 dlam = -rh ;
-        #   -dt - D_sl^-1 dlam_sl = -rh_sl
-        # eliminated with K = D_TR^-1 + G W^-1 G' (8x8 SPD, floored), k = K^-1 1, kap = 1'k:
-        #   dt = (vt + D_sl rh_sl - cw 1'K^-1 a) / (D_sl + cw^2 kap),  a = G W^-1 vL + rh
-        #   dlam = K^-1 a + cw dt k ;  dL = W^-1 (vL - G'dlam) ;  dlam_sl = cw 1'dlam - vt
-        WLi = 1.0 / qp.Wx[6:9]
-        YL = PENUM * WLi[None, :]                                  # G W^-1 (8x3)
-        GWG_tr = PENUM @ YL.T                                       # (8x8)
-        DinvT = np.where(D[0] > 0, 1.0 / np.maximum(D[0], 1e-300), 1e300)
-        kfl = 1e-12 * np.trace(GWG_tr)
-        Ktr = GWG_tr[None] + np.maximum(DinvT, kfl)[:, :, None] * np.eye(8)[None]
-        Ktr_inv = np.linalg.inv(Ktr)                                # (N+1,8,8)
-        kvec = Ktr_inv.sum(axis=2)                                  # K^-1 1
-        kap = kvec.sum(axis=1)
-        Dsl = D[1]
-        den = Dsl + qp.cw ** 2 * kap
-        Pm = Ktr_inv - qp.cw ** 2 * np.einsum('ka,kb->kab', kvec, kvec) / den[:, None, None]
-        ML = np.diag(WLi)[None] - np.einsum('ja,kjl,lb->kab', YL, Pm, YL)
-        Mfull = np.zeros((N + 1, 9, 9))
-        Mfull[:, np.arange(6), np.arange(6)] = 1.0 / qp.Wx[:6]
-        Mfull[:, 6:9, 6:9] = ML
-        # u blocks, computed stably (D can reach 1e15+): with K = D^-1 + G W^-1 G' (4x4 SPD),
-        # Phi_u^-1 = W^-1 - W^-1 G' K^-1 G W^-1 and Phi_u^-1 G' D = W^-1 G' K^-1 (push-through).
-        Wu_b = qp.Wu.reshape(nc, nupc)
-        Winv = np.zeros((N, nc, nupc, nupc)) + np.stack([np.diag(1.0 / Wu_b[i]) for i in range(nc)])[None]
-        if talos:
-            # CoP rows are bound rows on single coordinates: fold them into the diagonal
-            # (D <= 1/lo-side slack, bounded by the box width, so no cancellation)
-            dcop = D[3].sum(axis=3)                                   # (N, nc, 2)
-            for d in range(2):
-                Winv[:, :, d, d] = 1.0 / (Wu_b[None, :, d] + dcop[:, :, d])
-        Gw = np.einsum('kirm,kimn->kirn', qp.G, Winv[:, :, fo:fo + 3, fo:fo + 3])    # G W^-1 (N,nc,4,3)
-        Dinv_f = np.where(fm > 0, s[2] / np.where(fm > 0, lam[2], 1.0), 1.0)
-        GWG = np.einsum('kirn,kiqn->kirq', Gw, qp.G)
-        # floor on D^-1: at a zero force all four pyramid rows are active (degenerate, K -> rank 3);
-        # kernel KFLOOR_FR (1e-9; 1e-12 before round 2's TALOS weight cases)
-        kfloor = fric_floor * np.trace(GWG, axis1=2, axis2=3)[..., None] + 1e-300
-        Kf = GWG + np.maximum(Dinv_f, kfloor)[..., None] * np.eye(4)
-        Kf = np.where(fm[..., None] > 0, Kf, np.eye(4))                 # inactive contacts: identity
-        Gw = Gw * fm[..., None]
-        Kf_inv = np.linalg.inv(Kf)
-        Phiuinv = Winv.copy()
-        Phiuinv[:, :, fo:fo + 3, fo:fo + 3] -= np.einsum('kirn,kirq,kiqm->kinm', Gw, Kf_inv, Gw)
-        # S blocks
-        Sd = np.zeros((N + 2, 9, 9)); So = np.zeros((N + 1, 9, 9))
-        Sd[0] = Mfull[0]
-        Bblk = qp.Bm.reshape(N, 9, nc, nupc)
-        BPB = np.einsum('kaic,kicd,kbid->kab', Bblk, Phiuinv, Bblk)
-        Sd[1:N + 1] = np.einsum('kai,kij,kbj->kab', qp.A, Mfull[:N], qp.A) + BPB + Mfull[1:]
-        Sd[N + 1] = Mfull[N]
-        So[0] = Mfull[0] @ qp.A[0].T
-        So[1:N] = -np.einsum('kij,kbj->kib', Mfull[1:N], qp.A[1:N])
-        So[N] = -Mfull[N]
-        # block Cholesky: Lc[j] lower, Lo[j] = S_{j+1,j} Lc[j]^-T
-        Lc = np.zeros_like(Sd); Lo = np.zeros_like(So)
-        # tiny diagonal regularization of each Schur block: the last blocks are differences of
-        # O(M) numbers once the forces are pinned by active rows (cancellation), see DESIGN.md
-        for j in range(N + 2):
-            Sd[j] += reg * np.trace(Sd[j]) / 9 * np.eye(9)
-        Sh = Sd[0].copy()
-        for j in range(N + 2):
-            Lc[j] = _chol_floor(Sh, piv_floor * np.diag(Sd[j]))
-            if j < N + 1:
-                Lo[j] = np.linalg.solve(Lc[j], So[j]).T        # (S_{j,j+1})^T Lc^-T
-                Sh = Sd[j + 1] - Lo[j] @ Lo[j].T
-
-        def tr_local(vL, vt, rh_tr, rh_sl):
-            """(dL, dt, dlam_TR, dlam_sl) of the (L, t) block (see the factorization)."""
-            a = vL @ YL.T + rh_tr                                   # (N+1, 8)
-            ka = np.einsum('kab,kb->ka', Ktr_inv, a)
-            dt_ = (vt + Dsl * rh_sl - qp.cw * ka.sum(axis=1)) / den
-            dlt = ka + qp.cw * dt_[:, None] * kvec
-            dL = WLi[None, :] * (vL - dlt @ PENUM)
-            dls = qp.cw * dlt.sum(axis=1) - vt
-            return dL, dt_, dlt, dls
-
-        def u_local(vu, rh_f, rh_cp):
-            """(du, dlam_fric) of the control blocks: friction rows in push-through form, CoP
-            rows folded into the diagonal."""
-            vu = vu.reshape(N, nc, nupc).copy()
+        def system(s, lam, rdx, rdt, rdu, rde, rdi):
+            """Factorization of the Newton system at (s, lam); returns newton(rc, ...) and lin_res."""
+            D = [li / si * mk for li, si, mk in zip(lam, s, masks)]
+            # cap D on the rows handled in D-form (TR, slack, CoP): beyond ~1e12 x the stage
+            # curvature the products D * r lose all precision; the capped Newton step is an inexact
+            # Newton step on exact residuals (convergence is driven by the residuals)
+            dcap = dcap_rel * max(float(np.max(qp.Wx)), 1.0)
             if talos:
-                vu[:, :, 0:2] += -(D[3][..., 0] * rh_cp[..., 0] - D[3][..., 1] * rh_cp[..., 1])
-            du_ = np.einsum('kiab,kib->kia', Winv, vu)
-            vf = vu[:, :, fo:fo + 3]
-            z = np.einsum('kirn,kin->kir', Gw, vf) + rh_f
-            dlf = np.einsum('kirq,kiq->kir', Kf_inv, z) * fm
-            gl = np.einsum('kirm,kir->kim', qp.G, dlf)
-            du_[:, :, fo:fo + 3] = np.einsum('kiab,kib->kia', Winv[:, :, fo:fo + 3, fo:fo + 3], vf - gl)
-            return du_.reshape(N, nu), dlf
-
-        def phi_solve(vx, vt, vu):
-            """Phi^-1 (vx, vt, vu) (no row terms)."""
-            dx = vx / qp.Wx[None, :]
-            dL, dt_, _, _ = tr_local(vx[:, 6:9], vt, np.zeros((N + 1, 8)), np.zeros(N + 1))
-            dx[:, 6:9] = dL
-            du_, _ = u_local(vu, np.zeros((N, nc, 4)), np.zeros((N, nc, 2, 2)) if talos else None)
-            return dx, dt_, du_
-
-        def newton(rc, rdx=rdx, rdt=rdt, rdu=rdu, rde=rde, rdi=rdi):
-            rhat = [(ri - c / np.where(mk > 0, li, 1.0)) * mk for ri, c, li, mk in zip(rdi, rc, lam, masks)]
-            rcp = rhat[3] if talos else None
-            # particular solution w = Phi^-1 (r_d + G'D rhat): local solves with v = -r_d
-            wx = rdx / qp.Wx[None, :]
-            dL, dt0, _, _ = tr_local(-rdx[:, 6:9], -rdt, rhat[0], rhat[1])
-            wx[:, 6:9] = -dL
-            wt = -dt0
-            du0, _ = u_local(-rdu, rhat[2], rcp)
-            wu = -du0
-            rhs = rde - Ez(wx, wu)
-            # forward / backward block substitution
-            y = np.zeros((N + 2, 9))
+                D[3] = np.minimum(D[3], dcap)
+            # x/t block: Phi_LL, Phi_Lt, Phi_tt
+            # (L, t) block in push-through form.  Unknowns dL (3), dt, dlam_TR (8), dlam_sl:
+            #   W dL + G' dlam = vL ;  cw 1'dlam - dlam_sl = vt ;  G dL + cw 1 dt - D^-1 dlam = -rh ;
+            #   -dt - D_sl^-1 dlam_sl = -rh_sl
+            # eliminated with K = D_TR^-1 + G W^-1 G' (8x8 SPD, floored), k = K^-1 1, kap = 1'k:
+            #   dt = (vt + D_sl rh_sl - cw 1'K^-1 a) / (D_sl + cw^2 kap),  a = G W^-1 vL + rh
+            #   dlam = K^-1 a + cw dt k ;  dL = W^-1 (vL - G'dlam) ;  dlam_sl = cw 1'dlam - vt
+            WLi = 1.0 / qp.Wx[6:9]
+            YL = PENUM * WLi[None, :]                                  # G W^-1 (8x3)
+            GWG_tr = PENUM @ YL.T                                       # (8x8)
+            DinvT = np.where(D[0] > 0, 1.0 / np.maximum(D[0], 1e-300), 1e300)
+            kfl = 1e-12 * np.trace(GWG_tr)
+            Ktr = GWG_tr[None] + np.maximum(DinvT, kfl)[:, :, None] * np.eye(8)[None]
+            Ktr_inv = np.linalg.inv(Ktr)                                # (N+1,8,8)
+            kvec = Ktr_inv.sum(axis=2)                                  # K^-1 1
+            kap = kvec.sum(axis=1)
+            Dsl = D[1]
+            den = Dsl + qp.cw ** 2 * kap
+            Pm = Ktr_inv - qp.cw ** 2 * np.einsum('ka,kb->kab', kvec, kvec) / den[:, None, None]
+            ML = np.diag(WLi)[None] - np.einsum('ja,kjl,lb->kab', YL, Pm, YL)
+            Mfull = np.zeros((N + 1, 9, 9))
+            Mfull[:, np.arange(6), np.arange(6)] = 1.0 / qp.Wx[:6]
+            Mfull[:, 6:9, 6:9] = ML
+            # u blocks, computed stably (D can reach 1e15+): with K = D^-1 + G W^-1 G' (4x4 SPD),
+            # Phi_u^-1 = W^-1 - W^-1 G' K^-1 G W^-1 and Phi_u^-1 G' D = W^-1 G' K^-1 (push-through).
+            Wu_b = qp.Wu.reshape(nc, nupc)
+            Winv = np.zeros((N, nc, nupc, nupc)) + np.stack([np.diag(1.0 / Wu_b[i]) for i in range(nc)])[None]
+            if talos:
+                # CoP rows are bound rows on single coordinates: fold them into the diagonal
+                # (D <= 1/lo-side slack, bounded by the box width, so no cancellation)
+                dcop = D[3].sum(axis=3)                                   # (N, nc, 2)
+                for d in range(2):
+                    Winv[:, :, d, d] = 1.0 / (Wu_b[None, :, d] + dcop[:, :, d])
+            Gw = np.einsum('kirm,kimn->kirn', qp.G, Winv[:, :, fo:fo + 3, fo:fo + 3])    # G W^-1 (N,nc,4,3)
+            Dinv_f = np.where(fm > 0, s[2] / np.where(fm > 0, lam[2], 1.0), 1.0)
+            GWG = np.einsum('kirn,kiqn->kirq', Gw, qp.G)
+            # floor on D^-1: at a zero force all four pyramid rows are active (degenerate, K -> rank 3);
+            # kernel KFLOOR_FR (1e-9; 1e-12 before round 2's TALOS weight cases)
+            kfloor = fric_floor * np.trace(GWG, axis1=2, axis2=3)[..., None] + 1e-300
+            Kf = GWG + np.maximum(Dinv_f, kfloor)[..., None] * np.eye(4)
+            Kf = np.where(fm[..., None] > 0, Kf, np.eye(4))                 # inactive contacts: identity
+            Gw = Gw * fm[..., None]
+            Kf_inv = np.linalg.inv(Kf)
+            Phiuinv = Winv.copy()
+            Phiuinv[:, :, fo:fo + 3, fo:fo + 3] -= np.einsum('kirn,kirq,kiqm->kinm', Gw, Kf_inv, Gw)
+            # S blocks
+            Sd = np.zeros((N + 2, 9, 9)); So = np.zeros((N + 1, 9, 9))
+            Sd[0] = Mfull[0]
+            Bblk = qp.Bm.reshape(N, 9, nc, nupc)
+            BPB = np.einsum('kaic,kicd,kbid->kab', Bblk, Phiuinv, Bblk)
+            Sd[1:N + 1] = np.einsum('kai,kij,kbj->kab', qp.A, Mfull[:N], qp.A) + BPB + Mfull[1:]
+            Sd[N + 1] = Mfull[N]
+            So[0] = Mfull[0] @ qp.A[0].T
+            So[1:N] = -np.einsum('kij,kbj->kib', Mfull[1:N], qp.A[1:N])
+            So[N] = -Mfull[N]
+            # block Cholesky: Lc[j] lower, Lo[j] = S_{j+1,j} Lc[j]^-T
+            Lc = np.zeros_like(Sd); Lo = np.zeros_like(So)
+            # tiny diagonal regularization of each Schur block: the last blocks are differences of
+            # O(M) numbers once the forces are pinned by active rows (cancellation), see DESIGN.md
             for j in range(N + 2):
-                b = rhs[j] - (Lo[j - 1] @ y[j - 1] if j > 0 else 0)
-                y[j] = np.linalg.solve(Lc[j], b)
-            dnu = np.zeros((N + 2, 9))
-            for j in range(N + 1, -1, -1):
-                b = y[j] - (Lo[j].T @ dnu[j + 1] if j < N + 1 else 0)
-                dnu[j] = np.linalg.solve(Lc[j].T, b)
-            ex_, eu_ = ET(dnu)
-            # full direction from the local solves with v = -(r_d + E'dnu)
-            vx = -(rdx + ex_); vu = -(rdu + eu_)
-            dx = vx / qp.Wx[None, :]
-            dL, dt_, dlt, dls = tr_local(vx[:, 6:9], -rdt, rhat[0], rhat[1])
-            dx[:, 6:9] = dL
-            du, dlf = u_local(vu, rhat[2], rcp)
-            gz = Gz(dx, du, dt_)
-            dl = [dlt, dls, dlf]
-            if talos:
-                dl.append(D[3] * (gz[3] + rhat[3]) * masks[3])
-            ds = [(-ri - g) * mk for ri, g, mk in zip(rdi, gz, masks)]
-            return dx, dt_, du, dnu, dl, ds
+                Sd[j] += reg * np.trace(Sd[j]) / 9 * np.eye(9)
+            Sh = Sd[0].copy()
+            for j in range(N + 2):
+                Lc[j] = _chol_floor(Sh, piv_floor * np.diag(Sd[j]))
+                if j < N + 1:
+                    Lo[j] = np.linalg.solve(Lc[j], So[j]).T        # (S_{j,j+1})^T Lc^-T
+                    Sh = Sd[j + 1] - Lo[j] @ Lo[j].T
 
-        def max_step(v, dv, mk):
-            neg = (dv < 0) & (mk > 0)
-            if not np.any(neg):
-                return 1.0
-            return min(1.0, float(np.min(-v[neg] / dv[neg])))
+            def tr_local(vL, vt, rh_tr, rh_sl):
+                """(dL, dt, dlam_TR, dlam_sl) of the (L, t) block (see the factorization)."""
+                a = vL @ YL.T + rh_tr                                   # (N+1, 8)
+                ka = np.einsum('kab,kb->ka', Ktr_inv, a)
+                dt_ = (vt + Dsl * rh_sl - qp.cw * ka.sum(axis=1)) / den
+                dlt = ka + qp.cw * dt_[:, None] * kvec
+                dL = WLi[None, :] * (vL - dlt @ PENUM)
+                dls = qp.cw * dlt.sum(axis=1) - vt
+                return dL, dt_, dlt, dls
 
-        def lin_res(d, rc):
-            """Residual of the Newton system at direction d (the exact operators)."""
-            dx, dt_, du, dnu, dl, ds = d
-            gx_, gt_, gu_ = GT(dl)
-            ex_, eu_ = ET(dnu)
-            zx = np.zeros_like(dx); zu = np.zeros_like(du)
-            gz = Gz(dx, du, dt_)
-            return (qp.Wx * dx + ex_ + gx_ + rdx, gt_ + rdt, qp.Wu * du + eu_ + gu_ + rdu,
-                    Ez(dx, du) - Ez(zx, zu) + rde,
-                    [(g + dsi + ri) * mk for g, dsi, ri, mk in zip(gz, ds, rdi, masks)],
-                    [(si * dli + li * dsi + c) * mk for si, dli, li, dsi, c, mk in zip(s, dl, lam, ds, rc, masks)])
+            def u_local(vu, rh_f, rh_cp):
+                """(du, dlam_fric) of the control blocks: friction rows in push-through form, CoP
+                rows folded into the diagonal."""
+                vu = vu.reshape(N, nc, nupc).copy()
+                if talos:
+                    vu[:, :, 0:2] += -(D[3][..., 0] * rh_cp[..., 0] - D[3][..., 1] * rh_cp[..., 1])
+                du_ = np.einsum('kiab,kib->kia', Winv, vu)
+                vf = vu[:, :, fo:fo + 3]
+                z = np.einsum('kirn,kin->kir', Gw, vf) + rh_f
+                dlf = np.einsum('kirq,kiq->kir', Kf_inv, z) * fm
+                gl = np.einsum('kirm,kir->kim', qp.G, dlf)
+                du_[:, :, fo:fo + 3] = np.einsum('kiab,kib->kia', Winv[:, :, fo:fo + 3, fo:fo + 3], vf - gl)
+                return du_.reshape(N, nu), dlf
 
+            def phi_solve(vx, vt, vu):
+                """Phi^-1 (vx, vt, vu) (no row terms)."""
+                dx = vx / qp.Wx[None, :]
+                dL, dt_, _, _ = tr_local(vx[:, 6:9], vt, np.zeros((N + 1, 8)), np.zeros(N + 1))
+                dx[:, 6:9] = dL
+                du_, _ = u_local(vu, np.zeros((N, nc, 4)), np.zeros((N, nc, 2, 2)) if talos else None)
+                return dx, dt_, du_
+
+            def newton(rc, rdx=rdx, rdt=rdt, rdu=rdu, rde=rde, rdi=rdi):
+                rhat = [(ri - c / np.where(mk > 0, li, 1.0)) * mk for ri, c, li, mk in zip(rdi, rc, lam, masks)]
+                rcp = rhat[3] if talos else None
+                # particular solution w = Phi^-1 (r_d + G'D rhat): local solves with v = -r_d
+                wx = rdx / qp.Wx[None, :]
+                dL, dt0, _, _ = tr_local(-rdx[:, 6:9], -rdt, rhat[0], rhat[1])
+                wx[:, 6:9] = -dL
+                wt = -dt0
+                du0, _ = u_local(-rdu, rhat[2], rcp)
+                wu = -du0
+                rhs = rde - Ez(wx, wu)
+                # forward / backward block substitution
+                y = np.zeros((N + 2, 9))
+                for j in range(N + 2):
+                    b = rhs[j] - (Lo[j - 1] @ y[j - 1] if j > 0 else 0)
+                    y[j] = np.linalg.solve(Lc[j], b)
+                dnu = np.zeros((N + 2, 9))
+                for j in range(N + 1, -1, -1):
+                    b = y[j] - (Lo[j].T @ dnu[j + 1] if j < N + 1 else 0)
+                    dnu[j] = np.linalg.solve(Lc[j].T, b)
+                ex_, eu_ = ET(dnu)
+                # full direction from the local solves with v = -(r_d + E'dnu)
+                vx = -(rdx + ex_); vu = -(rdu + eu_)
+                dx = vx / qp.Wx[None, :]
+                dL, dt_, dlt, dls = tr_local(vx[:, 6:9], -rdt, rhat[0], rhat[1])
+                dx[:, 6:9] = dL
+                du, dlf = u_local(vu, rhat[2], rcp)
+                gz = Gz(dx, du, dt_)
+                dl = [dlt, dls, dlf]
+                if talos:
+                    dl.append(D[3] * (gz[3] + rhat[3]) * masks[3])
+                ds = [(-ri - g) * mk for ri, g, mk in zip(rdi, gz, masks)]
+                return dx, dt_, du, dnu, dl, ds
+
+            def lin_res(d, rc):
+                """Residual of the Newton system at direction d (the exact operators)."""
+                dx, dt_, du, dnu, dl, ds = d
+                gx_, gt_, gu_ = GT(dl)
+                ex_, eu_ = ET(dnu)
+                zx = np.zeros_like(dx); zu = np.zeros_like(du)
+                gz = Gz(dx, du, dt_)
+                return (qp.Wx * dx + ex_ + gx_ + rdx, gt_ + rdt, qp.Wu * du + eu_ + gu_ + rdu,
+                        Ez(dx, du) - Ez(zx, zu) + rde,
+                        [(g + dsi + ri) * mk for g, dsi, ri, mk in zip(gz, ds, rdi, masks)],
+                        [(si * dli + li * dsi + c) * mk for si, dli, li, dsi, c, mk in zip(s, dl, lam, ds, rc, masks)])
+            return newton, lin_res
+
+        newton, lin_res = system(s, lam, rdx, rdt, rdu, rde, rdi)
         rc_aff = [si * li * mk for si, li, mk in zip(s, lam, masks)]
         dx, dt_, du, dnu, dl, ds = newton(rc_aff)
         if init:
@@ -416,8 +437,51 @@ def solve(qp, eps=1e-11, max_iter=60, eta=0.999, verbose=False, reg=0.0, piv_flo
         x = x + a * dx; t = t + a * dt_; u = u + a * du; nu_ = nu_ + a * dnu
         s = [np.where(mk > 0, si + a * dsi, 1.0) for si, dsi, mk in zip(s, ds, masks)]
         lam = [(li + a * dli) * mk for li, dli, mk in zip(lam, dl, masks)]
-    return dict(x=x, u=u, t=t, nu=nu_, lam=lam, s=s, status=status, iters=it, hist=hist, merit=merit,
-                n_refine=n_refine)
+        last = (a, ds, dl)
+    out = dict(x=x, u=u, t=t, nu=nu_, lam=lam, s=s, status=status, iters=it, hist=hist, merit=merit,
+               n_refine=n_refine, polish=polish_log[-1]['status'] if polish_log else 0, polish_log=polish_log)
+    return out
+
+
+def _polish(qp, masks, x, u, t, nu_, s, lam, last, system, GT, ET, Ez, ineq_val, e_rhs, eps, talos, rel):
+    """Solution polishing (the reference's osqp setup has polish=True, src/scp_solver.py:62): the
+    equality-constrained QP on the active set guessed from the converged iterate, solved with one
+    Newton step of the same structured system.  Active set by the Tapia indicators of the last step
+    (s_k / s_{k-1} against lambda_k / lambda_{k-1}: on an active row s vanishes while lambda settles,
+    on an inactive one the reverse; lambda > s alone misreads rows where both are small).  Active
+    rows get s = rel * lambda (D = 1 / rel: the push-through blocks then floor D^-1 as in any
+    solve), inactive rows lambda = rel * s (D = rel), and the Newton step with sigma = 0 and a full
+    step gives the solution of the reduced KKT system.  Accepted (status 1) when every active row
+    keeps lambda >= -eps * scale_d and every inactive row s >= -eps * scale_p; otherwise -1 and the
+    interior-point solution stands."""
+    N = qp.N
+    a, ds, dl = last
+    s_prev = [np.where(mk > 0, si - a * dsi, 1.0) for si, dsi, mk in zip(s, ds, masks)]
+    l_prev = [(li - a * dli) * mk for li, dli, mk in zip(lam, dl, masks)]
+    act = [(mk > 0) & (si * lp < li * sp) for si, li, sp, lp, mk in zip(s, lam, s_prev, l_prev, masks)]
+    s1 = [np.where(ac, rel * li, si) for si, li, ac in zip(s, lam, act)]
+    l1 = [np.where(ac, li, rel * si) * mk for si, li, ac, mk in zip(s, lam, act, masks)]
+    gx, gt, gu = GT(l1)
+    ex, eu = ET(nu_)
+    rdx = qp.Wx * x + qp.qx + ex + gx
+    rdt = 1.0 + gt
+    rdu = qp.Wu * u + eu + gu
+    rde = Ez(x, u) - e_rhs
+    vals = ineq_val(x, u, t)
+    rdi = [(v + si) * mk for v, si, mk in zip(vals, s1, masks)]
+    newton, _ = system(s1, l1, rdx, rdt, rdu, rde, rdi)
+    dx, dt_, du, dnu, dlp, dsp = newton([si * li * mk for si, li, mk in zip(s1, l1, masks)])
+    x2, t2, u2, n2 = x + dx, t + dt_, u + du, nu_ + dnu
+    s2 = [np.where(mk > 0, si + dsi, 1.0) for si, dsi, mk in zip(s1, dsp, masks)]
+    l2 = [(li + dli) * mk for li, dli, mk in zip(l1, dlp, masks)]
+    scale_p = max(np.abs(Ez(x2, u2)).max(), np.abs(e_rhs).max(), 1.0)
+    scale_d = max(np.abs(qp.Wx * x2).max(), np.abs(qp.Wu * u2).max(), np.abs(qp.qx).max(), 1.0)
+    lmin = min(float(np.min(np.where(ac, li, np.inf))) for li, ac in zip(l2, act))
+    smin = min(float(np.min(np.where((mk > 0) & ~ac, -v, np.inf)))
+               for v, ac, mk in zip(ineq_val(x2, u2, t2), act, masks))
+    ok = lmin >= -eps * scale_d and smin >= -eps * scale_p
+    return dict(status=1 if ok else -1, x=x2, u=u2, t=t2, nu=n2, s=s2, lam=l2, lmin=lmin, smin=smin,
+                n_active=int(sum(a_.sum() for a_ in act)))
 
 
 def to_z(qp, sol):
