@@ -95,6 +95,8 @@ extern "C" int cmpc_load_qp(cmpc_handle h, int b, int n, int m, const double *P_
 
         // ---- cost: diagonal P, one Wx / Wu for all knots
         std::vector<double> pd(n, 0.0);
+        need(P_p[0] == 0, "P: invalid column pointers");
+        for (int j = 0; j < n; ++j) need(P_p[j + 1] >= P_p[j], "P: column pointers not monotone");
         for (int j = 0; j < n; ++j)
             for (int e = P_p[j]; e < P_p[j + 1]; ++e) {
                 need(P_i[e] >= 0 && P_i[e] < n, "P: row index out of range");
