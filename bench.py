@@ -27,7 +27,7 @@ Extra fields ("Measurement"):
                 time.  Its first QP launch has no Newton counts to group problems by.
   repeats       the timed region run 5 more times (median of 5); ``value`` is the first
                 region, as the bench contract asks.
-  qp_exit       QP exit-status histogram and refinement counts of the last timed step.
+  qp_exit       QP exit-status histogram, refinement and polishing counts of the last timed step.
   cpu_baseline  the oracle (numpy/scipy restatement of the reference path, OSQP algorithm at the
                 reference's eps 1e-7 with polish) on bounded samples, rank 0 at N = 1 only:
                 throughput over the box's CPU share, single-core latency and early exit.
@@ -65,6 +65,16 @@ def algorithmic_qp_bytes(N, ipm_iters_total, w, robot='solo12'):
     fact = s['L_f'] + 2 * s['a_k'] + s['n_k'] + s['m_k']
     solve = s['L_f'] + 1.5 * s['a_k'] + 6 * s['m_k'] + 3 * s['n_k']
     return N * w * (fact + 2 * solve) * ipm_iters_total
+
+
+def polish_step_fraction(robot='solo12'):
+    """A polishing step (qp_ipm.hip phase_polish_prep: one factorization and one solve of the reduced
+    KKT system, no corrector) in units of a Newton step's algorithmic bytes (one factorization, two
+    solves)."""
+    s = per_knot_sizes(robot)
+    fact = s['L_f'] + 2 * s['a_k'] + s['n_k'] + s['m_k']
+    solve = s['L_f'] + 1.5 * s['a_k'] + 6 * s['m_k'] + 3 * s['n_k']
+    return (fact + solve) / (fact + 2 * solve)
 
 
 def compulsory_qp_bytes(N, ipm_iters_total, w, robot='solo12'):
@@ -291,6 +301,9 @@ def main():
     ipm_total = solver.qp_iterations_total()        # IPM iterations of the last step, all problems
     _, _, qst, _ = solver.qp_solution(with_y=False)
     merit, nref = solver.qp_info()
+    _, qpol = solver.qp_exit()
+    # Newton-step units of the last step: the Newton steps plus the polishing steps tried
+    ipm_units = ipm_total + float((qpol != 0).sum()) * polish_step_fraction(pb.robot)
     rep_ms = []
     if not args.no_extras:   # SURVEY.md 8d's median of 5, beside the contract's single timed region
         for _ in range(5):
@@ -306,8 +319,8 @@ def main():
     w = 8 if args.precision in ('fp64', 'f64', 'float64') else 4
     n_steps = max(tim['iterations'], 1)
     qp_mean_s = tim['qp_ms'] / 1e3 / n_steps
-    achieved = algorithmic_qp_bytes(args.N, ipm_total, w, pb.robot) / qp_mean_s / 1e9
-    compulsory = compulsory_qp_bytes(args.N, ipm_total, w, pb.robot) / qp_mean_s / 1e9
+    achieved = algorithmic_qp_bytes(args.N, ipm_units, w, pb.robot) / qp_mean_s / 1e9
+    compulsory = compulsory_qp_bytes(args.N, ipm_units, w, pb.robot) / qp_mean_s / 1e9
     traffic, traffic_prov = None, None
     metric_config = (args.config, args.N, nb, w) == ('trot', 100, 1024, 8)
     if metric_config:   # the PMC summary was measured on the metric config only
@@ -335,7 +348,8 @@ def main():
         'qp_ipm_iterations_mean': ipm_total / nb,
         'qp_exit': {'status_counts': {str(int(a)): int(b) for a, b in zip(u, c)},
                     'merit_max': float(merit.max()), 'refined_problems': int((nref > 0).sum()),
-                    'refine_steps': int(nref.sum())},
+                    'refine_steps': int(nref.sum()), 'polish_accepted': int((qpol > 0).sum()),
+                    'polish_rejected': int((qpol < 0).sum())},
         'roofline': {'kernel': solver.qp_kernel(), 'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                      'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
                      'traffic_provenance': traffic_prov,

@@ -40,7 +40,8 @@ class Params(ctypes.Structure):
 class QPSettings(ctypes.Structure):
     _fields_ = [('max_iter', ctypes.c_int32), ('eps_abs', ctypes.c_double), ('eps_rel', ctypes.c_double),
                 ('step_fraction', ctypes.c_double), ('init_floor_s', ctypes.c_double),
-                ('init_floor_l', ctypes.c_double), ('waves_per_problem', ctypes.c_int32)]
+                ('init_floor_l', ctypes.c_double), ('waves_per_problem', ctypes.c_int32),
+                ('polish_eps', ctypes.c_double)]
 
 
 class Gait(ctypes.Structure):
@@ -75,7 +76,7 @@ EXPORTS = ['cmpc_create', 'cmpc_destroy', 'cmpc_last_error', 'cmpc_version', 'cm
            'cmpc_get_solution', 'cmpc_get_iteration_log', 'cmpc_get_timing', 'cmpc_timing_begin',
            'cmpc_timing_end', 'cmpc_get_qp_iterations_total', 'cmpc_debug_stamps', 'cmpc_get_qp_kernel', 'cmpc_set_scp_mode',
            'cmpc_get_linearization_point', 'cmpc_interpolate', 'cmpc_generate_contact_plans',
-           'cmpc_upload_states', 'cmpc_get_contact_plans', 'cmpc_get_warm_start', 'cmpc_get_qp_info', 'cmpc_get_qp_tail',
+           'cmpc_upload_states', 'cmpc_get_contact_plans', 'cmpc_get_warm_start', 'cmpc_get_qp_info', 'cmpc_get_qp_exit',
            'cmpc_comm_get_unique_id', 'cmpc_comm_init', 'cmpc_comm_destroy', 'cmpc_comm_bcast_params',
            'cmpc_comm_allreduce_max', 'cmpc_comm_gather_solution', 'cmpc_load_qp', 'cmpc_get_iteration_history',
            'cmpc_get_accepted', 'cmpc_host_register', 'cmpc_host_unregister',
@@ -136,7 +137,7 @@ def load():
         'cmpc_get_contact_plans': (i32, [h, vp, vp, vp]),
         'cmpc_get_warm_start': (i32, [h, vp, vp]),
         'cmpc_get_qp_info': (i32, [h, vp, vp]),
-        'cmpc_get_qp_tail': (i32, [h, vp]),
+        'cmpc_get_qp_exit': (i32, [h, vp, vp]),
         'cmpc_comm_get_unique_id': (i32, [vp]),
         'cmpc_comm_init': (i32, [h, i32, i32, vp]),
         'cmpc_comm_destroy': (i32, [h]),
@@ -245,7 +246,7 @@ class Solver:
 
     # ---- setup
     def set_qp_settings(self, max_iter=None, eps_abs=None, eps_rel=None, step_fraction=None, init_floor_s=None,
-                        init_floor_l=None, waves_per_problem=None):
+                        init_floor_l=None, waves_per_problem=None, polish_eps=None):
         s = QPSettings()
         self.lib.cmpc_default_qp_settings(self.prec, ctypes.byref(s))
         if max_iter is not None: s.max_iter = int(max_iter)
@@ -255,6 +256,7 @@ class Solver:
         if init_floor_s is not None: s.init_floor_s = float(init_floor_s)
         if init_floor_l is not None: s.init_floor_l = float(init_floor_l)
         if waves_per_problem is not None: s.waves_per_problem = int(waves_per_problem)
+        if polish_eps is not None: s.polish_eps = float(polish_eps)
         self._chk(self.lib.cmpc_set_qp_settings(self.h, ctypes.byref(s)), 'cmpc_set_qp_settings')
 
     def set_params(self, params):
@@ -425,12 +427,18 @@ class Solver:
         self._chk(self.lib.cmpc_get_qp_info(self.h, _ptr(merit), _ptr(nref)), 'cmpc_get_qp_info')
         return merit, nref
 
+    def qp_exit(self):
+        """Per problem: (tail, polish) of the last QP -- the Newton steps that ran on the whole grouped
+        workgroup after the hand-over (0: solved on its own wave only), and the solution polishing
+        (1 accepted, -1 rejected, 0 not tried)."""
+        tail = np.zeros(self.B, np.int32); pol = np.zeros(self.B, np.int32)
+        if _VARIANT and not hasattr(self.lib, 'cmpc_get_qp_exit'):   # an older diagnostic build
+            return tail, pol
+        self._chk(self.lib.cmpc_get_qp_exit(self.h, _ptr(tail), _ptr(pol)), 'cmpc_get_qp_exit')
+        return tail, pol
+
     def qp_tail(self):
-        """Per problem, the Newton steps of the last QP that ran on the whole grouped workgroup after
-        the hand-over (0: solved on its own wave only)."""
-        out = np.zeros(self.B, np.int32)
-        self._chk(self.lib.cmpc_get_qp_tail(self.h, _ptr(out)), 'cmpc_get_qp_tail')
-        return out
+        return self.qp_exit()[0]
 
     def solution(self, pinned=False, with_ks=True):
         """Accepted X, U (and with_ks K, Sigma) plus the per-problem SCP state.  pinned=True writes

@@ -21,8 +21,8 @@ template <typename T, int R> __global__ void k_linearize(DevBuf<T>, int);
 template <typename T, int R> __global__ void k_lin_knots(DevBuf<T>, int, int);
 template <typename T, int R> __global__ void k_cov_scan(DevBuf<T>, int);
 template <typename T, int R, bool FULL> __global__ void k_assemble(DevBuf<T>, int);
-template <typename T, int R, int NTT> __global__ void k_qp_ipm(DevBuf<T>, int, int, T, T, T, T, T);
-template <typename T, int R, int P> __global__ void k_qp_group(DevBuf<T>, const int *, int, int, int, T, T, T, T, T);
+template <typename T, int R, int NTT> __global__ void k_qp_ipm(DevBuf<T>, int, int, T, T, T, T, T, T);
+template <typename T, int R, int P> __global__ void k_qp_group(DevBuf<T>, const int *, int, int, int, T, T, T, T, T, T);
 template <typename T> __global__ void k_qp_order(DevBuf<T>, int, int, int *);
 size_t ipm_group_lds_bytes(int N, int prec_bytes, int P);
 int ipm_pair_max_batch();
@@ -142,6 +142,11 @@ int qp_group(cmpc_handle h) {
         if (e[0] == '4' && h->N >= 40) P = 4;
     }
     if (ipm_group_lds_bytes(h->N, esz, P) > cap) P = 2;
+    // TALOS pairs (k_qp_group<double, 1, 2> with hand-over: TALOS batches of N < 40, no BASELINE
+    // configuration) stopped on a memory-aperture fault in round 4 (N = 40, 9 problems) that the
+    // instrumented build (per-phase progress trace) did not reproduce; they run one wave per problem
+    // until it is found ("Grouped workgroups").  Solo12 pairs and all quads are unaffected.
+    if (P == 2 && h->robot == CMPC_ROBOT_TALOS) return 0;
     return ipm_group_lds_bytes(h->N, esz, P) <= cap ? P : 0;
 }
 
@@ -159,6 +164,20 @@ int qp_pair_share() {
 double qp_step_fraction(cmpc_handle h) {
     if (h->qs.step_fraction > 0) return h->qs.step_fraction;
     return h->robot == 1 ? 0.995 : 0.999;
+}
+
+// Polishing tolerance: the setting, or (< 0) the robot's.  Measured on the CPU mirror of the kernel
+// (oracle/ipm_mirror.py, problems of the metric batch and of C4; DESIGN.md, "Polishing"): Solo12
+// trot N=100 polishes at 1e-9 on every slow problem sampled (7 -> 5-6 Newton steps, solutions to the
+// exact minimizer, where the unpolished 1e-10 solve stops up to 9e-5 away); at 1e-8 a fifth of them
+// guess the active set wrong.  TALOS N=200 polishes at 1e-7 on every problem sampled (14-17 -> 13).
+// fp32 (C3, two Newton steps at 1e-6) is not polished.
+double qp_polish_eps(cmpc_handle h) {
+    if (h->prec != CMPC_PREC_F64) return 0.0;
+    if (const char *e = std::getenv("CMPC_QP_POLISH_EPS"))   // diagnostic override (A/B runs)
+        return std::atof(e);
+    if (h->qs.polish_eps >= 0) return h->qs.polish_eps;
+    return h->robot == 1 ? 1e-7 : 1e-9;
 }
 
 // Covariance scan placement.  Sigma feeds only the chance-constraint back-off of stochastic
@@ -270,11 +289,11 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
             if (P == 4)
                 hipLaunchKernelGGL((k_qp_group<T, R, 4>), dim3(ng), dim3(256), lds, h->stream, d, (const int *)h->qp_order,
                                    only_active, qp_pair_share(), h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), eta,
-                                   T(h->qs.init_floor_s), T(h->qs.init_floor_l));
+                                   T(h->qs.init_floor_s), T(h->qs.init_floor_l), T(qp_polish_eps(h)));
             else
                 hipLaunchKernelGGL((k_qp_group<T, R, 2>), dim3(ng), dim3(128), lds, h->stream, d, (const int *)h->qp_order,
                                    only_active, qp_pair_share(), h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), eta,
-                                   T(h->qs.init_floor_s), T(h->qs.init_floor_l));
+                                   T(h->qs.init_floor_s), T(h->qs.init_floor_l), T(qp_polish_eps(h)));
             if (h->scan_pending) {
                 HIPCHK(hipStreamWaitEvent(h->stream, h->ev_scan, 0));
                 h->scan_pending = false;
@@ -295,15 +314,15 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
         if (nt == 256)
             hipLaunchKernelGGL((k_qp_ipm<T, R, 256>), dim3(B), dim3(256), lds, h->stream, d, only_active,
                                h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), eta,
-                               T(h->qs.init_floor_s), T(h->qs.init_floor_l));
+                               T(h->qs.init_floor_s), T(h->qs.init_floor_l), T(qp_polish_eps(h)));
         else if (nt == 128)
             hipLaunchKernelGGL((k_qp_ipm<T, R, 128>), dim3(B), dim3(128), lds, h->stream, d, only_active,
                                h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), eta,
-                               T(h->qs.init_floor_s), T(h->qs.init_floor_l));
+                               T(h->qs.init_floor_s), T(h->qs.init_floor_l), T(qp_polish_eps(h)));
         else
             hipLaunchKernelGGL((k_qp_ipm<T, R, 64>), dim3(B), dim3(64), lds, h->stream, d, only_active,
                                h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), eta,
-                               T(h->qs.init_floor_s), T(h->qs.init_floor_l));
+                               T(h->qs.init_floor_s), T(h->qs.init_floor_l), T(qp_polish_eps(h)));
         if (h->scan_pending) {   // join behind the QP
             HIPCHK(hipStreamWaitEvent(h->stream, h->ev_scan, 0));
             h->scan_pending = false;
@@ -562,6 +581,7 @@ void reset_scp(cmpc_handle h, const int32_t *class_id) {
     // index (k_qp_order), not by counts learned on whatever the handle solved before
     HIPCHK(hipMemsetAsync(h->qp_iters, 0, (size_t)h->B * 4, h->stream));
     HIPCHK(hipMemsetAsync(h->qp_tail, 0, (size_t)h->B * 4, h->stream));
+    HIPCHK(hipMemsetAsync(h->qp_polish, 0, (size_t)h->B * 4, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
 }
 
@@ -606,6 +626,7 @@ int cmpc_default_qp_settings(int precision, cmpc_qp_settings *s) {
     s->init_floor_s = 0.1;
     s->init_floor_l = 0.1;
     s->waves_per_problem = 0;
+    s->polish_eps = -1.0;   // the robot's (qp_polish_eps)
     return 0;
 }
 
@@ -674,6 +695,7 @@ int cmpc_create(cmpc_handle *out, int device, int robot, int N, int max_batch, i
         h->qp_merit = h->dalloc(Bm * e);
         h->qp_nref = h->dalloc(Bm * 4);
         h->qp_tail = h->dalloc(Bm * 4);
+        h->qp_polish = h->dalloc(Bm * 4);
         h->ws_stride = ipm_workspace_elems(N, robot);
         h->ws = h->dalloc(Bm * h->ws_stride * e);
         h->scp = h->dalloc(Bm * sizeof(ScpState));
@@ -1189,11 +1211,11 @@ int cmpc_get_qp_info(cmpc_handle h, double *merit, int32_t *n_refine) {
     });
 }
 
-int cmpc_get_qp_tail(cmpc_handle h, int32_t *tail_steps) {
+int cmpc_get_qp_exit(cmpc_handle h, int32_t *tail_steps, int32_t *polish) {
     return guard(h, [&] {
         need(h->B > 0, "no problems uploaded");
-        need(tail_steps != nullptr, "null output buffer");
-        from_dev_raw(h, tail_steps, h->qp_tail, (size_t)h->B * 4);
+        if (tail_steps) from_dev_raw(h, tail_steps, h->qp_tail, (size_t)h->B * 4);
+        if (polish) from_dev_raw(h, polish, h->qp_polish, (size_t)h->B * 4);
     });
 }
 

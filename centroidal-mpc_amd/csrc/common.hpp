@@ -89,6 +89,7 @@ template <typename T> struct DevBuf {
     T *qp_merit;                    // (B) final merit (residual / tolerance; <= 1 when solved)
     int32_t *qp_nref;               // (B) refinement steps taken
     int32_t *qp_tail;               // (B) Newton steps run on the whole workgroup after a hand-over (k_qp_group)
+    int32_t *qp_polish;             // (B) solution polishing: 1 accepted, -1 rejected, 0 not tried
     // IPM workspace
     T *ws;
     size_t ws_stride;               // elements per problem

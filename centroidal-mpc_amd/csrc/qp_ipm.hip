@@ -65,7 +65,7 @@ template <int ROBOT> struct Ws {
         s = 0, l = s + NI, x = l + NI, u = x + 9, t = u + NU, nu = t + 1, rdx = nu + 9, rdt = rdx + 9,
         rdu = rdt + 1, rde = rdu + NU, rdi = rde + 9, facx = rdi + NI, facu = facx + FX, wx = facu + NC * FU,
         wt = wx + 9, wu = wt + 1, dx = wu + NU, dt = dx + 9, du = dt + 1, ds = du + NU, dl = ds + NI,
-        dsa = dl + NI, dla = dsa + NI, dn0 = dla + NI, NF = dn0 + 9
+        dsa = dl + NI, dla = dsa + NI, dn0 = dla + NI, ub = dn0 + 9, NF = ub + NU
     };
     // Schur blocks (block-major 9x9): S_jj -> I_j, and S_{j,j+1} -> X_{j+1} / Y_j (tw_factor_ends);
     // four-wave workgroups also the fill factors H_j and the separator scratch (schur_pt.hpp)
@@ -416,7 +416,8 @@ __device__ __forceinline__ void contact_wd(const Ctx<T, ROBOT> &C, int c, bool a
 // (1) residuals of knot k; returns norm contributions
 // prim / dual / comp: residual maxima; mu: complementarity sum over cnt rows; sp / sd: scales of
 // the relative tolerances
-template <typename T, int ROBOT> struct Norms { T prim, dual, comp, mu, sp, sd, lmax, cnt; };
+template <typename T, int ROBOT> struct Norms { T prim, dual, comp, mu, sp, sd, lmax, cnt, smin, lmin; };
+template <typename T> __device__ __forceinline__ T big_value() { return std::numeric_limits<T>::max(); }
 
 // Per-knot phases follow load -> compute -> store: every store into the workspace comes after
 // the last load (the compiler cannot move a load above a store that may alias it, so interleaving
@@ -528,6 +529,8 @@ __device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<
         nm.comp = fmax(nm.comp, c);
         mug += c;
         nm.lmax = fmax(nm.lmax, pr ? T(lr) : T(0));
+        nm.smin = fmin(nm.smin, pr ? T(sr) : big_value<T>());   // (the polished iterate's sign check)
+        nm.lmin = fmin(nm.lmin, pr ? T(lr) : big_value<T>());
         return pr ? lr : A(0);
     };
     nm.cnt += T((PART != 1 ? 9 : 0) + (hu && PART != 0 ? 4 * (1 + Robot<ROBOT>::COP) * __builtin_popcount(msk) : 0));
@@ -1944,6 +1947,78 @@ template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_update(const C
 }
 
 
+// ---- solution polishing (the reference's osqp.setup(..., polish=True), src/scp_solver.py:62)
+// Once the iterate meets the polishing tolerance, the equality-constrained QP on the guessed active
+// set is solved with one more Newton step of the same structured system (oracle/ipm_mirror.py
+// _polish is the CPU counterpart, step for step):
+//   * active set from the Tapia indicators of the last step: row r is active when s_r / s_r,prev <
+//     lambda_r / lambda_r,prev (s vanishing while lambda settles; lambda > s alone misreads rows
+//     where both are small, e.g. the weakly active friction rows that hold the Newton tail), with
+//     s_prev = s - alpha ds, lambda_prev = lambda - alpha dlambda from the last step's direction
+//     (still in the ds / dl fields) and step length;
+//   * active rows get s = rel lambda (D = 1 / rel, so D^-1 meets the push-through floors), inactive
+//     rows lambda = rel s (D = rel: the row drops out); the residual pass, the Newton step with
+//     sigma = 0 (predictor semantics) and a full step (alpha = 1) then give the reduced KKT solution;
+//   * a residual pass verifies it: merit <= 1 at eps and s, lambda >= -tolerance on every row, i.e.
+//     an exact KKT point (the minimizer); otherwise the iterate before the polish is restored and
+//     the interior-point iterations go on.
+// Backups while the polish runs: s, lambda in the ds, dl fields (whose last direction the
+// classification has consumed), x, t, u in wx, wt, ub, nu in dn0 (fields no other phase uses then).
+constexpr double POLISH_REL = 1e-14;
+template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_polish_prep(const Ctx<T, ROBOT> &C, int k, T alpha) {
+    constexpr int NI = Rows<ROBOT>::NI;
+    const int N = C.N;
+    const unsigned msk = C.cmask(k);
+    T s[NI], l[NI], ds[NI], dl[NI], x[9], u[NU], n1[9], n0[9];
+    ldv(C.kv(WF(s), k), s);
+    ldv(C.kv(WF(l), k), l);
+    ldv(C.kv(WF(ds), k), ds);
+    ldv(C.kv(WF(dl), k), dl);
+    ldv(C.var_x(k), x);
+    ldv(C.var_u(k), u);   // k = N: padding column
+    ldv(C.bv(WF(nu), 1 + k), n1);
+    ldv(C.bv(WF(nu), 0), n0);
+    const T t = C.kv(WF(t), k)[0];
+    const T rel = T(POLISH_REL);
+    T s1[NI], l1[NI];
+#pragma unroll
+    for (int r = 0; r < NI; ++r) {
+        const bool pr = Ctx<T, ROBOT>::present_m(k < N ? msk : 0u, r);
+        const T sp = s[r] - alpha * ds[r], lp = l[r] - alpha * dl[r];
+        const bool act = pr && s[r] * lp < l[r] * sp;
+        s1[r] = act ? rel * l[r] : s[r];
+        l1[r] = pr ? (act ? l[r] : rel * s[r]) : l[r];
+    }
+    stv(C.kv(WF(ds), k), s);
+    stv(C.kv(WF(dl), k), l);
+    stv(C.kv(WF(wx), k), x);
+    C.kv(WF(wt), k)[0] = t;
+    stv(C.kv(WF(ub), k), u);
+    stv(C.bv(WF(dn0), 1 + k), n1);
+    if (k == 0) stv(C.bv(WF(dn0), 0), n0);
+    stv(C.kv(WF(s), k), s1);
+    stv(C.kv(WF(l), k), l1);
+}
+// the iterate before the polish, back from its backups (a rejected polish)
+template <typename T, int ROBOT> __device__ PHASE_ATTR void phase_polish_rollback(const Ctx<T, ROBOT> &C, int k) {
+    constexpr int NI = Rows<ROBOT>::NI;
+    T s[NI], l[NI], x[9], u[NU], n1[9], n0[9];
+    ldv(C.kv(WF(ds), k), s);
+    ldv(C.kv(WF(dl), k), l);
+    ldv(C.kv(WF(wx), k), x);
+    ldv(C.kv(WF(ub), k), u);
+    ldv(C.bv(WF(dn0), 1 + k), n1);
+    ldv(C.bv(WF(dn0), 0), n0);
+    const T t = C.kv(WF(wt), k)[0];
+    stv(C.kv(WF(s), k), s);
+    stv(C.kv(WF(l), k), l);
+    stv(C.var_x(k), x);
+    if (k < C.N) stv(C.var_u(k), u);
+    C.kv(WF(t), k)[0] = t;
+    stv(C.bv(WF(nu), 1 + k), n1);
+    if (k == 0) stv(C.bv(WF(nu), 0), n0);
+}
+
 // initialization step: full Newton step for z and nu; s = h - gz at the new z; lambda += dlambda.
 // vmax receives (max -s, max -lambda) over this knot's rows.
 // Starting point after the initialization step: s = h - g'z at the new z for the present rows
@@ -2099,7 +2174,9 @@ template <int G> constexpr bool split_knots() { return G >= 256; }
 // complementarity mean and row count.
 template <typename T> struct IpmState {
     int status, it, stall, n_refine, yielded, resume, tail;
+    int ptried, polish;   // polishing tried / its outcome (1 accepted, -1 rejected)
     T mu_prev, merit, prim_prev, mu, cnt;
+    T alpha_last;         // step length of the last Newton step (the polish's active-set guess)
 #ifdef CMPC_STAMPS
     unsigned long long t_acc[12];
 #endif
@@ -2107,9 +2184,10 @@ template <typename T> struct IpmState {
 template <typename T> __device__ __forceinline__ IpmState<T> ipm_state0() {
     IpmState<T> S;
     S.status = CMPC_QP_MAX_ITER;
-    S.it = S.stall = S.n_refine = S.yielded = S.resume = S.tail = 0;
+    S.it = S.stall = S.n_refine = S.yielded = S.resume = S.tail = S.ptried = S.polish = 0;
     S.mu_prev = T(-1);
     S.merit = S.prim_prev = S.mu = S.cnt = T(0);
+    S.alpha_last = T(1);
 #ifdef CMPC_STAMPS
     for (int i = 0; i < 12; ++i) S.t_acc[i] = 0;
 #endif
@@ -2227,7 +2305,7 @@ __device__ __forceinline__ void group_done(LdsT<int> *gf, int w) {
 template <typename T, int ROBOT, int G, int WG>
 __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT> &C, int b, IpmState<T> &S,
                                          const IpmLds<T> &L, int max_iter, T eps_abs, T eps_rel, T eta,
-                                         LdsT<int> *gf = nullptr, int gP = 0) {
+                                         T polish_eps, LdsT<int> *gf = nullptr, int gP = 0) {
     const int tid = threadIdx.x & (G - 1), N = C.N, K1 = N + 1, NB = N + 2, NBm = NB / 2;
     (void)b;
 #ifdef CMPC_STAMPS
@@ -2242,21 +2320,30 @@ __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT>
 #define STAMP(i) do { } while (0)
 #endif
     int status = S.status, it = S.it, stall = S.stall, n_refine = S.n_refine;
-    T mu_prev = S.mu_prev, merit = S.merit, prim_prev = S.prim_prev;
+    T mu_prev = S.mu_prev, merit = S.merit, prim_prev = S.prim_prev, alpha_last = S.alpha_last;
     bool resume = S.resume != 0;
     S.resume = 0;
+    // pm: 0 a Newton step; 1 the polishing step (its own residual pass and Newton system, full step);
+    // 2 the residual pass that verifies the polished iterate (accepted: solved; rejected: rolled back
+    // and iteration `it` redone as a Newton step, the stopping-test state restored)
+    int pm = 0, stall_s = 0;
+    T mu_prev_s = T(0), prim_prev_s = T(0);
     // it == 0 is the initialization step: one full Newton step from s = lambda = 1 gives an
     // equality-feasible least-squares start; s and lambda are then floored row by row (Solo12)
     // or shifted by 1 + the largest violation (TALOS), see init_s_knot.
-    for (it = S.it; it <= max_iter; ++it) {
-        const bool init = (it == 0);
+    for (it = S.it; it <= max_iter;) {
+        const bool init = (it == 0) && pm == 0;
         T mu, cnt;   // complementarity mean and row count of this iteration's residual pass
         if (resume) {   // handed over after this iteration's stopping test (k_qp_group)
             resume = false;
             mu = S.mu;
             cnt = S.cnt;
         } else {
-        Norms<T, ROBOT> nm{0, 0, 0, 0, 0, 0, 0, 0};
+        if (pm == 1) {   // polishing: active-set guess, backups, the reduced system's s and lambda
+            for (int k = tid; k < K1; k += G) phase_polish_prep<T, ROBOT>(C, k, alpha_last);
+            gsync<G, WG>();
+        }
+        Norms<T, ROBOT> nm{0, 0, 0, 0, 0, 0, 0, 0, big_value<T>(), big_value<T>()};
         if constexpr (split_knots<G>()) {   // a thread pair per knot: state part | contact part
             // (the part is the wave's: a uniform branch)
             if (__builtin_amdgcn_readfirstlane(tid) < 128) {
@@ -2276,8 +2363,31 @@ __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT>
         mu = sm2[0] / fmax(sm2[1], T(1));
         cnt = sm2[1];
         const T ep = eps_abs + eps_rel * sp, ed = eps_abs + eps_rel * sdd;
+        if (pm == 2) {   // the polished iterate: an exact KKT point within eps, or back to the old one
+            T mn[2] = {nm.smin, nm.lmin};
+            block_reduce<T, G, 2, 2, WG>(mn, L.red);
+            const T mp = fmax(prim / ep, fmax(dual / ed, comp / ed));
+            if (mp <= T(1) && mn[0] >= -ep && mn[1] >= -ed) {
+                merit = mp;
+                status = CMPC_QP_SOLVED;
+                S.polish = 1;
+                break;
+            }
+            S.polish = -1;
+            for (int k = tid; k < K1; k += G) phase_polish_rollback<T, ROBOT>(C, k);
+            gsync<G, WG>();
+            stall = stall_s;
+            mu_prev = mu_prev_s;
+            prim_prev = prim_prev_s;
+            pm = 0;
+            continue;   // iteration `it` again, as a Newton step
+        }
+        if (pm == 1) goto newton_system;
         merit = fmax(prim / ep, fmax(dual / ed, comp / ed));
         if (!(merit == merit) || !(mu == mu)) { status = CMPC_QP_NONFINITE; break; }
+        stall_s = stall;
+        mu_prev_s = mu_prev;
+        prim_prev_s = prim_prev;
         if (!init) {
             if (merit <= T(1)) { status = CMPC_QP_SOLVED; break; }
             // primal infeasibility (Farkas, OSQP's test on the diverging multipliers), checked once
@@ -2301,6 +2411,14 @@ __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT>
             if (stall >= 3 && merit <= T(1e3)) { status = CMPC_QP_SOLVED_INACCURATE; break; }
         }
         if (it == max_iter) break;
+        // polishing once the iterate meets polish_eps (after at least one Newton step past the
+        // initialization, whose direction the active-set guess reads)
+        if (polish_eps > T(0) && !S.ptried && it > 1 &&
+            fmax(prim / (polish_eps * (T(1) + sp)), fmax(dual, comp) / (polish_eps * (T(1) + sdd))) <= T(1)) {
+            S.ptried = 1;
+            pm = 1;
+            continue;
+        }
         // k_qp_group: every other problem of the workgroup has stopped, so this one continues on
         // all waves from here (the residual pass of this iteration is in the workspace)
         if (gf && group_handover(gf, gP, (int)(threadIdx.x >> 6), it)) {
@@ -2311,6 +2429,7 @@ __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT>
             break;
         }
         }   // (residual pass and stopping test)
+    newton_system:
         // ---- Phi factors and the predictor's particular solution (knot-local), then the S blocks
         // and the predictor's Schur right-hand side
         if constexpr (split_knots<G>()) {
@@ -2378,7 +2497,9 @@ __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT>
             gsync<G, WG>();
         }
         STAMP(3);
-        // ---- predictor (affine) and corrector
+        // ---- predictor (affine) and corrector; the initialization step and the polishing step take the
+        // predictor's direction alone (full stores into the affine fields)
+        const bool one_step = init || pm == 1;
         T sigma_mu = T(0);
         T alpha = T(1);
         for (int corr = 0; corr < 2; ++corr) {
@@ -2406,17 +2527,17 @@ __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT>
             T am[1] = {T(1)}, mus[3] = {T(0), T(0), T(0)};
             if constexpr (split_knots<G>()) {
                 if (__builtin_amdgcn_readfirstlane(tid) < 128) {
-                    for (int k = tid & 127; k < K1; k += 128) am[0] = fmin(am[0], phase_dz<T, ROBOT, 0>(C, k, corr, init, sigma_mu, mus));
+                    for (int k = tid & 127; k < K1; k += 128) am[0] = fmin(am[0], phase_dz<T, ROBOT, 0>(C, k, corr, one_step, sigma_mu, mus));
                 } else {
-                    for (int k = tid & 127; k < K1; k += 128) am[0] = fmin(am[0], phase_dz<T, ROBOT, 1>(C, k, corr, init, sigma_mu, mus));
+                    for (int k = tid & 127; k < K1; k += 128) am[0] = fmin(am[0], phase_dz<T, ROBOT, 1>(C, k, corr, one_step, sigma_mu, mus));
                 }
             } else {
-                for (int k = tid; k < K1; k += G) am[0] = fmin(am[0], phase_dz<T, ROBOT>(C, k, corr, init, sigma_mu, mus));
+                for (int k = tid; k < K1; k += G) am[0] = fmin(am[0], phase_dz<T, ROBOT>(C, k, corr, one_step, sigma_mu, mus));
             }
             block_reduce<T, G, 1, 2, WG>(am, L.red);
             STAMP(7);
             alpha = am[0];
-            if (init) break;
+            if (one_step) break;
             if (corr == 0) {   // Mehrotra centering from the affine step's complementarity
                 block_reduce<T, G, 3, 0, WG>(mus, L.red);
                 const T mu_aff = (mus[0] + alpha * (mus[1] + alpha * mus[2])) / fmax(cnt, T(1));
@@ -2441,12 +2562,21 @@ __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT>
                 for (int k = tid; k < K1; k += G) phase_init_shift<T, ROBOT>(C, k, sh_s, sh_l);
             }
             gsync<G, WG>();
+            ++it;
+            continue;
+        }
+        if (pm == 1) {   // the reduced system's solution: a full step, verified by the next residual pass
+            for (int k = tid; k < K1; k += G) phase_update<T, ROBOT>(C, k, T(1), true);
+            gsync<G, WG>();
+            pm = 2;
             continue;
         }
         alpha = fmin(T(1), eta * alpha);
         for (int k = tid; k < K1; k += G) phase_update<T, ROBOT>(C, k, alpha);
         gsync<G, WG>();
         STAMP(8);
+        alpha_last = alpha;
+        ++it;
     }
     S.status = status;
     S.it = it;
@@ -2455,6 +2585,7 @@ __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT>
     S.mu_prev = mu_prev;
     S.merit = merit;
     S.prim_prev = prim_prev;
+    S.alpha_last = alpha_last;
 #undef STAMP
 }
 
@@ -2482,6 +2613,7 @@ __device__ __forceinline__ void ipm_finish(const DevBuf<T> &d, const Ctx<T, ROBO
         d.qp_merit[b] = S.merit;
         d.qp_nref[b] = S.n_refine;
         d.qp_tail[b] = S.tail;
+        d.qp_polish[b] = S.polish;
 #ifdef CMPC_STAMPS
         for (int i = 0; i < 9; ++i) d.stamps[(size_t)b * 16 + i] = S.t_acc[i];   // 9..11: k_linearize, 12..15: tw_factor_ends
 #endif
@@ -2491,7 +2623,7 @@ __device__ __forceinline__ void ipm_finish(const DevBuf<T> &d, const Ctx<T, ROBO
 // One workgroup per problem: one, two or four waves (cmpc_api.cpp qp_waves).
 template <typename T, int ROBOT, int NTT>
 __global__ void __launch_bounds__(NTT, NTT == 128 ? QP_MIN_WAVES_2W : QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int only_active, int max_iter, T eps_abs, T eps_rel,
-                                               T eta, T floor_s, T floor_l) {
+                                               T eta, T floor_s, T floor_l, T polish_eps) {
     extern __shared__ __attribute__((aligned(16))) unsigned char dsmem[];
     const int b = blockIdx.x;
     if (b >= d.B) return;
@@ -2527,7 +2659,7 @@ __global__ void __launch_bounds__(NTT, NTT == 128 ? QP_MIN_WAVES_2W : QP_MIN_WAV
     }
     IpmState<T> S = ipm_state0<T>();
     ipm_start<T, ROBOT, NTT, NTT>(d, C, b);
-    ipm_loop<T, ROBOT, NTT, NTT>(d, C, b, S, L, max_iter, eps_abs, eps_rel, eta, nullptr);
+    ipm_loop<T, ROBOT, NTT, NTT>(d, C, b, S, L, max_iter, eps_abs, eps_rel, eta, polish_eps);
     ipm_finish<T, ROBOT, NTT>(d, C, b, S);
     // Covariance scans of a deterministic batch (cmpc_api.cpp launch_phase): a workgroup whose QP
     // has finished takes scan jobs from the counter until none is left, so the scans fill the
@@ -2579,7 +2711,7 @@ template <typename T> struct GroupLds {
 template <typename T, int ROBOT, int P>
 __global__ void __launch_bounds__(64 * P, 1) k_qp_group(DevBuf<T> d, const int *order, int only_active, int share,
                                                         int max_iter, T eps_abs, T eps_rel, T eta, T floor_s,
-                                                        T floor_l) {
+                                                        T floor_l, T polish_eps) {
     extern __shared__ __attribute__((aligned(16))) unsigned char dsmem[];
     using GL = GroupLds<T>;
     constexpr int WG = 64 * P;
@@ -2615,7 +2747,7 @@ __global__ void __launch_bounds__(64 * P, 1) k_qp_group(DevBuf<T> d, const int *
         L.red = (T *)(after_vec(R) + GL::RING + GL::SH);
         IpmState<T> S = ipm_state0<T>();
         ipm_start<T, ROBOT, 64, WG>(d, C, b);
-        ipm_loop<T, ROBOT, 64, WG>(d, C, b, S, L, max_iter, eps_abs, eps_rel, eta, share ? gf : nullptr, P);
+        ipm_loop<T, ROBOT, 64, WG>(d, C, b, S, L, max_iter, eps_abs, eps_rel, eta, polish_eps, share ? gf : nullptr, P);
         if (S.yielded) {
             if (lane == 0) {
                 Ss = S;
@@ -2663,7 +2795,7 @@ __global__ void __launch_bounds__(64 * P, 1) k_qp_group(DevBuf<T> d, const int *
 #ifdef CMPC_STAMPS
         const unsigned long long tb0 = __builtin_amdgcn_s_memtime();
 #endif
-        ipm_loop<T, ROBOT, WG, WG>(d, C, b2, S, L, max_iter, eps_abs, eps_rel, eta);
+        ipm_loop<T, ROBOT, WG, WG>(d, C, b2, S, L, max_iter, eps_abs, eps_rel, eta, polish_eps);
         S.tail = S.it - it0;
         ipm_finish<T, ROBOT, WG>(d, C, b2, S);
 #ifdef CMPC_STAMPS
@@ -2753,11 +2885,11 @@ template <typename T> __global__ void __launch_bounds__(1024) k_qp_order(DevBuf<
 }
 
 #define INST(T, R)                                                                       \
-    template __global__ void k_qp_ipm<T, R, 64>(DevBuf<T>, int, int, T, T, T, T, T);     \
-    template __global__ void k_qp_ipm<T, R, 128>(DevBuf<T>, int, int, T, T, T, T, T);    \
-    template __global__ void k_qp_ipm<T, R, 256>(DevBuf<T>, int, int, T, T, T, T, T);    \
-    template __global__ void k_qp_group<T, R, 2>(DevBuf<T>, const int *, int, int, int, T, T, T, T, T); \
-    template __global__ void k_qp_group<T, R, 4>(DevBuf<T>, const int *, int, int, int, T, T, T, T, T);
+    template __global__ void k_qp_ipm<T, R, 64>(DevBuf<T>, int, int, T, T, T, T, T, T);     \
+    template __global__ void k_qp_ipm<T, R, 128>(DevBuf<T>, int, int, T, T, T, T, T, T);    \
+    template __global__ void k_qp_ipm<T, R, 256>(DevBuf<T>, int, int, T, T, T, T, T, T);    \
+    template __global__ void k_qp_group<T, R, 2>(DevBuf<T>, const int *, int, int, int, T, T, T, T, T, T); \
+    template __global__ void k_qp_group<T, R, 4>(DevBuf<T>, const int *, int, int, int, T, T, T, T, T, T);
 INST(double, 0)
 INST(double, 1)
 INST(float, 0)

@@ -118,6 +118,13 @@ typedef struct {
      * per-knot phases on two waves, the Schur recurrence on the first); 0 (default) picks 2 when
      * two waves per problem still fit the device in one round (2 B <= 4 x CUs) and N + 1 > 64 */
     int32_t waves_per_problem;
+    /* solution polishing, as the reference's OSQP setup (polish=True, src/scp_solver.py:62): once
+     * the iterate meets this tolerance (relative and absolute, like eps), the equality-constrained
+     * QP on the guessed active set is solved with one more factorization; accepted when the
+     * polished point meets eps with s, lambda >= 0 (then it is the exact minimizer), else the
+     * interior-point iterations go on.  < 0 (default): the robot's (fp64 Solo12 1e-9, TALOS 1e-7;
+     * fp32 off); 0: off */
+    double polish_eps;
 } cmpc_qp_settings;
 
 /* Per-phase device timings of the last cmpc_scp_iterate (milliseconds, HIP events). */
@@ -220,10 +227,12 @@ int cmpc_get_qp_solution(cmpc_handle h, double *z, double *y, int32_t *status, i
 /* Per-problem exit data of the last QP solve: final merit (<= 1 when solved) and the number of
  * iterative-refinement steps taken (B entries each; NULL skips). */
 int cmpc_get_qp_info(cmpc_handle h, double *merit, int32_t *n_refine);
-/* Per problem, the Newton steps of the last QP solve that ran on the whole workgroup after the
- * problem was handed over (grouped kernel k_qp_group: the last problem of a group, once the others
- * have stopped); 0 for problems solved on their own waves only.  B entries. */
-int cmpc_get_qp_tail(cmpc_handle h, int32_t *tail_steps);
+/* Per problem (B entries each; NULL skips): tail_steps, the Newton steps of the last QP solve that
+ * ran on the whole workgroup after the problem was handed over (grouped kernel k_qp_group: the last
+ * problem of a group, once the others have stopped; 0 for problems solved on their own waves only);
+ * polish, the solution polishing of that solve (1 accepted: the returned solution is the polished
+ * one; -1 tried and rejected; 0 not tried). */
+int cmpc_get_qp_exit(cmpc_handle h, int32_t *tail_steps, int32_t *polish);
 /* The accepted iterate of each problem (X, U) with that iteration's LQR gains and covariances.
  * Reference mode serves K and Sigma from the live linearization arrays, which every iteration
  * recomputes bit-identically (quirk Q1; the reference keeps references to that iteration's

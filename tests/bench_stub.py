@@ -76,6 +76,9 @@ class StubSolver:
     def qp_info(self):
         return np.full(self.B, 0.5), np.zeros(self.B, np.int32)
 
+    def qp_exit(self):
+        return np.zeros(self.B, np.int32), np.zeros(self.B, np.int32)
+
     def solve_scp(self, fixed_iters=False):
         self.scp_iterate()
         return 1
