@@ -52,7 +52,7 @@ static void create_validation() {
     CHECK(cmpc_create(&h, -1, 0, 20, 4, CMPC_PREC_F64) != 0 && h == nullptr);    // device id
     cmpc_qp_settings s;
     CHECK(cmpc_default_qp_settings(CMPC_PREC_F64, nullptr) != 0);
-    CHECK(cmpc_default_qp_settings(CMPC_PREC_F64, &s) == 0 && s.eps_abs == 1e-10 && s.polish_eps < 0);
+    CHECK(cmpc_default_qp_settings(CMPC_PREC_F64, &s) == 0 && s.eps_abs == 0.0 && s.polish_eps < 0);
 }
 
 static void device_paths(cmpc_handle h) {

@@ -132,8 +132,16 @@ int qp_waves(cmpc_handle h) {
 int qp_group(cmpc_handle h) {
     const int w = qp_waves(h);
     if (w != 1 || h->B < 2 || h->B > ipm_pair_max_batch() || h->prec != CMPC_PREC_F64) return 0;
-    if (const char *e = std::getenv("CMPC_QP_PAIR"))
-        if (e[0] == '0') return 0;
+    // Off by default since round 4: with this round's kernel changes the fused grouped kernel
+    // (one-wave loop and the all-wave tail in one code object, ~600 SGPR and 200-480 VGPR spills)
+    // stopped on memory-aperture faults on the GPU -- k_qp_group<double, 1, 2> shared and
+    // k_qp_group<double, 0, 4> even unshared, i.e. running only the one-wave loop that k_qp_ipm<.., 64>
+    // runs without fault on the same batch ("Grouped workgroups").  CMPC_QP_PAIR=1 (shared)
+    // or 2 (unshared) selects it for diagnostics.
+    {
+        const char *e = std::getenv("CMPC_QP_PAIR");
+        if (!e || (e[0] != '1' && e[0] != '2')) return 0;
+    }
     const size_t cap = 160 * 1024 - 1024;
     const int esz = (int)h->esz();
     int P = h->N >= 40 && ipm_group_lds_bytes(h->N, esz, 4) <= cap ? 4 : 2;
@@ -166,18 +174,26 @@ double qp_step_fraction(cmpc_handle h) {
     return h->robot == 1 ? 0.995 : 0.999;
 }
 
-// Polishing tolerance: the setting, or (< 0) the robot's.  Measured on the CPU mirror of the kernel
-// (oracle/ipm_mirror.py, problems of the metric batch and of C4; DESIGN.md, "Polishing"): Solo12
-// trot N=100 polishes at 1e-9 on every slow problem sampled (7 -> 5-6 Newton steps, solutions to the
-// exact minimizer, where the unpolished 1e-10 solve stops up to 9e-5 away); at 1e-8 a fifth of them
-// guess the active set wrong.  TALOS N=200 polishes at 1e-7 on every problem sampled (14-17 -> 13).
-// fp32 (C3, two Newton steps at 1e-6) is not polished.
+// Stopping tolerances: the settings, or (0) the robot's.  fp64: Solo12 1e-9 with complementarity
+// against the primal scale, TALOS 1e-10 (qp_ipm.hip COMP_PRIMAL_SCALE); fp32 1e-6.
+double qp_eps_default(cmpc_handle h) {
+    if (h->prec != CMPC_PREC_F64) return 1e-6;
+    return h->robot == 1 ? 1e-10 : 1e-9;
+}
+double qp_eps_abs(cmpc_handle h) { return h->qs.eps_abs > 0 ? h->qs.eps_abs : qp_eps_default(h); }
+double qp_eps_rel(cmpc_handle h) { return h->qs.eps_rel > 0 ? h->qs.eps_rel : qp_eps_default(h); }
+
+// Polishing tolerance: the setting, or (< 0) the robot's.  Solo12 polishes at 1e-8 (10x its eps):
+// on the GPU at the metric config the guess from 1e-9 was right on 296 problems and wrong on 4,
+// the slowest ones, where a rejected polish only adds a step (gpurun_out r04e, DESIGN.md
+// "Polishing"); TALOS N=200 at 1e-7 (15.4 -> 13.0 Newton steps on C4, 499 of 512 accepted).
+// fp32 (C3) is not polished.
 double qp_polish_eps(cmpc_handle h) {
     if (h->prec != CMPC_PREC_F64) return 0.0;
     if (const char *e = std::getenv("CMPC_QP_POLISH_EPS"))   // diagnostic override (A/B runs)
         return std::atof(e);
     if (h->qs.polish_eps >= 0) return h->qs.polish_eps;
-    return h->robot == 1 ? 1e-7 : 1e-9;
+    return h->robot == 1 ? 1e-7 : 1e-8;
 }
 
 // Covariance scan placement.  Sigma feeds only the chance-constraint back-off of stochastic
@@ -288,11 +304,11 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
             const unsigned ng = (unsigned)((B + P - 1) / P);
             if (P == 4)
                 hipLaunchKernelGGL((k_qp_group<T, R, 4>), dim3(ng), dim3(256), lds, h->stream, d, (const int *)h->qp_order,
-                                   only_active, qp_pair_share(), h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), eta,
+                                   only_active, qp_pair_share(), h->qs.max_iter, T(qp_eps_abs(h)), T(qp_eps_rel(h)), eta,
                                    T(h->qs.init_floor_s), T(h->qs.init_floor_l), T(qp_polish_eps(h)));
             else
                 hipLaunchKernelGGL((k_qp_group<T, R, 2>), dim3(ng), dim3(128), lds, h->stream, d, (const int *)h->qp_order,
-                                   only_active, qp_pair_share(), h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), eta,
+                                   only_active, qp_pair_share(), h->qs.max_iter, T(qp_eps_abs(h)), T(qp_eps_rel(h)), eta,
                                    T(h->qs.init_floor_s), T(h->qs.init_floor_l), T(qp_polish_eps(h)));
             if (h->scan_pending) {
                 HIPCHK(hipStreamWaitEvent(h->stream, h->ev_scan, 0));
@@ -313,15 +329,15 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
         }
         if (nt == 256)
             hipLaunchKernelGGL((k_qp_ipm<T, R, 256>), dim3(B), dim3(256), lds, h->stream, d, only_active,
-                               h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), eta,
+                               h->qs.max_iter, T(qp_eps_abs(h)), T(qp_eps_rel(h)), eta,
                                T(h->qs.init_floor_s), T(h->qs.init_floor_l), T(qp_polish_eps(h)));
         else if (nt == 128)
             hipLaunchKernelGGL((k_qp_ipm<T, R, 128>), dim3(B), dim3(128), lds, h->stream, d, only_active,
-                               h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), eta,
+                               h->qs.max_iter, T(qp_eps_abs(h)), T(qp_eps_rel(h)), eta,
                                T(h->qs.init_floor_s), T(h->qs.init_floor_l), T(qp_polish_eps(h)));
         else
             hipLaunchKernelGGL((k_qp_ipm<T, R, 64>), dim3(B), dim3(64), lds, h->stream, d, only_active,
-                               h->qs.max_iter, T(h->qs.eps_abs), T(h->qs.eps_rel), eta,
+                               h->qs.max_iter, T(qp_eps_abs(h)), T(qp_eps_rel(h)), eta,
                                T(h->qs.init_floor_s), T(h->qs.init_floor_l), T(qp_polish_eps(h)));
         if (h->scan_pending) {   // join behind the QP
             HIPCHK(hipStreamWaitEvent(h->stream, h->ev_scan, 0));
@@ -620,8 +636,8 @@ const char *cmpc_last_error(cmpc_handle h) { return h ? h->err.c_str() : "null h
 int cmpc_default_qp_settings(int precision, cmpc_qp_settings *s) {
     if (!s) return -1;
     s->max_iter = precision == CMPC_PREC_F64 ? 60 : 40;
-    s->eps_abs = precision == CMPC_PREC_F64 ? 1e-10 : 1e-6;
-    s->eps_rel = precision == CMPC_PREC_F64 ? 1e-10 : 1e-6;
+    s->eps_abs = 0.0;   // the robot's (qp_eps_default)
+    s->eps_rel = 0.0;
     s->step_fraction = 0.0;     // the robot's default, qp_step_fraction
     s->init_floor_s = 0.1;
     s->init_floor_l = 0.1;

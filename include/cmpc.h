@@ -106,8 +106,9 @@ typedef struct {
 /* QP solver settings (defaults by cmpc_default_qp_settings) */
 typedef struct {
     int32_t max_iter;       /* interior-point iterations (default 60) */
-    double eps_abs;         /* absolute tolerance (fp64 default 1e-10, fp32 1e-6) */
-    double eps_rel;         /* relative tolerance (fp64 default 1e-10, fp32 1e-6) */
+    double eps_abs;         /* absolute tolerance; 0 (default): the robot's -- fp64 Solo12 1e-9 (its
+                             * complementarity measured against the primal scale), TALOS 1e-10; fp32 1e-6 */
+    double eps_rel;         /* relative tolerance; 0 (default): as eps_abs */
     double step_fraction;   /* fraction-to-boundary in (0, 1); 0 (default) picks the robot's:
                              * Solo12 0.999, TALOS 0.995 (same-box measured) */
     /* Solo12 starting point: after the least-squares initialization step, s and lambda are
@@ -122,7 +123,7 @@ typedef struct {
      * the iterate meets this tolerance (relative and absolute, like eps), the equality-constrained
      * QP on the guessed active set is solved with one more factorization; accepted when the
      * polished point meets eps with s, lambda >= 0 (then it is the exact minimizer), else the
-     * interior-point iterations go on.  < 0 (default): the robot's (fp64 Solo12 1e-9, TALOS 1e-7;
+     * interior-point iterations go on.  < 0 (default): the robot's (fp64 Solo12 1e-8, TALOS 1e-7;
      * fp32 off); 0: off */
     double polish_eps;
 } cmpc_qp_settings;

@@ -91,6 +91,12 @@ INIT_FLOOR = 0.1          # s floor of the Solo12 starting point
 INIT_FLOOR_L = 0.1        # lambda floor
 
 
+def robot_defaults(qp):
+    """The kernel's default fp64 stopping and polishing tolerances for the QP's robot (cmpc_api.cpp
+    qp_eps_default / qp_polish_eps): Solo12 eps 1e-9, polish 1e-8; TALOS 1e-10, 1e-7."""
+    return (1e-9, 1e-8) if qp.robot == 'solo12' else (1e-10, 1e-7)
+
+
 def solve(qp, eps=1e-11, max_iter=60, eta=0.999, verbose=False, reg=0.0, piv_floor=1e-13, dcap_rel=1e12,
           refine_alpha=0.5, refine_merit=1e6, eps_pinf=1e-4, init_floor=INIT_FLOOR,
           init_floor_l=INIT_FLOOR_L, fric_floor=1e-9, polish=False, polish_eps=None, polish_rel=1e-14):
@@ -195,12 +201,21 @@ def solve(qp, eps=1e-11, max_iter=60, eta=0.999, verbose=False, reg=0.0, piv_flo
         prim = max(np.abs(rde).max(), max(np.maximum(v * mk, 0).max() for v, mk in zip(vals, masks)))
         dual = max(np.abs(rdx).max(), np.abs(rdt).max(), np.abs(rdu).max())
         comp = max((si * li * mk).max() for si, li, mk in zip(s, lam, masks))
-        scale_p = max(np.abs(Ez(x, u)).max(), np.abs(e_rhs).max(), 1.0)
-        scale_d = max(np.abs(qp.Wx * x).max(), np.abs(qp.Wu * u).max(), np.abs(qp.qx).max(), 1.0)
+        # the kernel's scales (qp_ipm.hip resid_knot: nm.sp, nm.sd): primal -- the dynamics and
+        # boundary rows' terms and every present inequality row's |g'z| and |h|; dual -- every term
+        # of the dual rows (W z, q, E' nu, G' lambda)
+        ineq_sc = max(float(np.max(np.where(mk > 0, np.maximum(np.abs(v + h), np.abs(np.broadcast_to(h, v.shape))), 0)))
+                      for v, h, mk in zip(vals, hs, masks))
+        scale_p = max(np.abs(Ez(x, u)).max(), np.abs(e_rhs).max(), np.abs(x[0]).max(), np.abs(x[N]).max(), ineq_sc, 1.0)
+        scale_d = max(np.abs(qp.Wx * x).max(), np.abs(qp.qx).max(), np.abs(ex).max(), np.abs(gx).max(),
+                      np.abs(qp.Wu * u).max(), np.abs(eu).max(), np.abs(gu).max(), 1.0)
+        # complementarity against the primal scale on Solo12, the dual scale on TALOS (qp_ipm.hip
+        # COMP_PRIMAL_SCALE)
+        scale_c = scale_d if talos else scale_p
         hist.append((it, prim, dual, comp, mu_))
         if verbose:
             print('it %2d prim %.2e dual %.2e comp %.2e mu %.2e' % (it, prim, dual, comp, mu_))
-        merit = max(prim / (eps * scale_p), dual / (eps * scale_d), comp / (eps * scale_d))
+        merit = max(prim / (eps * scale_p), dual / (eps * scale_d), comp / (eps * scale_c))
         if not (merit == merit):
             status = -10
             break

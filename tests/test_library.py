@@ -43,5 +43,7 @@ def test_default_qp_settings():
     lib = _lib.load()
     s = _lib.QPSettings()
     assert lib.cmpc_default_qp_settings(0, s) == 0
-    assert s.eps_abs == 1e-10 and s.eps_rel == 1e-10 and s.max_iter > 0 and s.waves_per_problem == 0
-    assert lib.cmpc_default_qp_settings(1, s) == 0 and s.eps_abs == 1e-6
+    # tolerances 0 = the robot's (cmpc_api.cpp qp_eps_default), polishing < 0 = the robot's
+    assert s.eps_abs == 0.0 and s.eps_rel == 0.0 and s.max_iter > 0 and s.waves_per_problem == 0
+    assert s.polish_eps < 0
+    assert lib.cmpc_default_qp_settings(1, s) == 0 and s.eps_abs == 0.0
