@@ -21,7 +21,9 @@ template <typename T, int R> __global__ void k_linearize(DevBuf<T>, int);
 template <typename T, int R> __global__ void k_lin_knots(DevBuf<T>, int, int);
 template <typename T, int R> __global__ void k_cov_scan(DevBuf<T>, int);
 template <typename T, int R, bool FULL> __global__ void k_assemble(DevBuf<T>, int);
-template <typename T, int R, int NTT> __global__ void k_qp_ipm(DevBuf<T>, int, int, T, T, T, T, T, T);
+template <typename T, int R, int NTT, int MODE> __global__ void k_qp_ipm(DevBuf<T>, int, int, T, T, T, T, T, T, int *);
+template <typename T> __global__ void k_qp_split(DevBuf<T>, int, int, int *);
+size_t ipm_state_bytes(int prec_bytes);
 template <typename T, int R, int P> __global__ void k_qp_group(DevBuf<T>, const int *, int, int, int, T, T, T, T, T, T);
 template <typename T> __global__ void k_qp_order(DevBuf<T>, int, int, int *);
 size_t ipm_group_lds_bytes(int N, int prec_bytes, int P);
@@ -163,6 +165,19 @@ int qp_group(cmpc_handle h) {
 int qp_pair_share() {
     const char *e = std::getenv("CMPC_QP_PAIR");
     return e && e[0] == '2' ? 0 : 1;
+}
+
+// Split QP launches (k_qp_ipm MODE 1 head + MODE 2 tail): for fp64 batches of one wave per problem
+// that fill the device (B > CUs, so two waves per problem do not fit one round), the slowest
+// problems' last Newton steps run on four waves (two below N = 40) in a second launch, one problem
+// per CU, once every other problem has finished (k_qp_split picks the yield iteration from the
+// previous launch's Newton counts).  Round 4's replacement for the grouped kernel (qp_group).
+// CMPC_QP_SPLIT=0 turns it off.  Returns the tail launch's waves per problem, or 0.
+int qp_split(cmpc_handle h) {
+    if (h->prec != CMPC_PREC_F64 || qp_waves(h) != 1 || h->B <= h->n_cu || qp_group(h)) return 0;
+    if (const char *e = std::getenv("CMPC_QP_SPLIT"))
+        if (e[0] == '0') return 0;
+    return h->N >= 40 ? 4 : 2;
 }
 
 // QP step fraction: the setting, or (0) the robot's. Same-box A/B, bench lines A B A B:
@@ -317,9 +332,10 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
             break;
         }
         const size_t lds = ipm_lds_bytes(h->N, (int)sizeof(T), nt);
-        const void *fn = nt == 256   ? reinterpret_cast<const void *>(&k_qp_ipm<T, R, 256>)
-                         : nt == 128 ? reinterpret_cast<const void *>(&k_qp_ipm<T, R, 128>)
-                                     : reinterpret_cast<const void *>(&k_qp_ipm<T, R, 64>);
+        const int tw = qp_split(h);
+        const void *fn = nt == 256   ? reinterpret_cast<const void *>(&k_qp_ipm<T, R, 256, 0>)
+                         : nt == 128 ? reinterpret_cast<const void *>(&k_qp_ipm<T, R, 128, 0>)
+                                     : reinterpret_cast<const void *>(&k_qp_ipm<T, R, 64, 0>);
         HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         if (h->scan_deferred) {   // the scans run in the QP's workgroups (one-wave kernel only)
             need(nt == 64, "internal: QP scan jobs need the one-wave kernel");
@@ -327,18 +343,42 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
             d.scan_ctr = (unsigned *)h->scan_ctr;
             h->scan_deferred = false;
         }
+        const T ea = T(qp_eps_abs(h)), er = T(qp_eps_rel(h)), fs = T(h->qs.init_floor_s), fl = T(h->qs.init_floor_l),
+                pe = T(qp_polish_eps(h));
+        if constexpr (sizeof(T) == 8) {
+            if (tw) {   // split launches: head (one wave per problem, the slowest leave), tail
+                int *sp = (int *)h->qp_split;
+                hipLaunchKernelGGL((k_qp_split<T>), dim3(1), dim3(1024), 0, h->stream, d, only_active, h->n_cu, sp);
+                hipLaunchKernelGGL((k_qp_ipm<T, R, 64, 1>), dim3(B), dim3(64), lds, h->stream, d, only_active,
+                                   h->qs.max_iter, ea, er, eta, fs, fl, pe, sp);
+                DevBuf<T> dt = d;
+                dt.scan_ctr = nullptr;
+                const size_t lt = ipm_lds_bytes(h->N, (int)sizeof(T), 64 * tw);
+                const void *ft = tw == 4 ? reinterpret_cast<const void *>(&k_qp_ipm<T, R, 256, 2>)
+                                         : reinterpret_cast<const void *>(&k_qp_ipm<T, R, 128, 2>);
+                HIPCHK(hipFuncSetAttribute(ft, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lt));
+                if (tw == 4)
+                    hipLaunchKernelGGL((k_qp_ipm<T, R, 256, 2>), dim3(B), dim3(256), lt, h->stream, dt, only_active,
+                                       h->qs.max_iter, ea, er, eta, fs, fl, pe, sp);
+                else
+                    hipLaunchKernelGGL((k_qp_ipm<T, R, 128, 2>), dim3(B), dim3(128), lt, h->stream, dt, only_active,
+                                       h->qs.max_iter, ea, er, eta, fs, fl, pe, sp);
+                if (h->scan_pending) {
+                    HIPCHK(hipStreamWaitEvent(h->stream, h->ev_scan, 0));
+                    h->scan_pending = false;
+                }
+                break;
+            }
+        }
         if (nt == 256)
-            hipLaunchKernelGGL((k_qp_ipm<T, R, 256>), dim3(B), dim3(256), lds, h->stream, d, only_active,
-                               h->qs.max_iter, T(qp_eps_abs(h)), T(qp_eps_rel(h)), eta,
-                               T(h->qs.init_floor_s), T(h->qs.init_floor_l), T(qp_polish_eps(h)));
+            hipLaunchKernelGGL((k_qp_ipm<T, R, 256, 0>), dim3(B), dim3(256), lds, h->stream, d, only_active,
+                               h->qs.max_iter, ea, er, eta, fs, fl, pe, nullptr);
         else if (nt == 128)
-            hipLaunchKernelGGL((k_qp_ipm<T, R, 128>), dim3(B), dim3(128), lds, h->stream, d, only_active,
-                               h->qs.max_iter, T(qp_eps_abs(h)), T(qp_eps_rel(h)), eta,
-                               T(h->qs.init_floor_s), T(h->qs.init_floor_l), T(qp_polish_eps(h)));
+            hipLaunchKernelGGL((k_qp_ipm<T, R, 128, 0>), dim3(B), dim3(128), lds, h->stream, d, only_active,
+                               h->qs.max_iter, ea, er, eta, fs, fl, pe, nullptr);
         else
-            hipLaunchKernelGGL((k_qp_ipm<T, R, 64>), dim3(B), dim3(64), lds, h->stream, d, only_active,
-                               h->qs.max_iter, T(qp_eps_abs(h)), T(qp_eps_rel(h)), eta,
-                               T(h->qs.init_floor_s), T(h->qs.init_floor_l), T(qp_polish_eps(h)));
+            hipLaunchKernelGGL((k_qp_ipm<T, R, 64, 0>), dim3(B), dim3(64), lds, h->stream, d, only_active,
+                               h->qs.max_iter, ea, er, eta, fs, fl, pe, nullptr);
         if (h->scan_pending) {   // join behind the QP
             HIPCHK(hipStreamWaitEvent(h->stream, h->ev_scan, 0));
             h->scan_pending = false;
@@ -712,6 +752,8 @@ int cmpc_create(cmpc_handle *out, int device, int robot, int N, int max_batch, i
         h->qp_nref = h->dalloc(Bm * 4);
         h->qp_tail = h->dalloc(Bm * 4);
         h->qp_polish = h->dalloc(Bm * 4);
+        h->qp_state = h->dalloc(Bm * ipm_state_bytes((int)e));
+        h->qp_split = h->dalloc((Bm + 2) * 4);
         h->ws_stride = ipm_workspace_elems(N, robot);
         h->ws = h->dalloc(Bm * h->ws_stride * e);
         h->scp = h->dalloc(Bm * sizeof(ScpState));
@@ -1457,8 +1499,10 @@ int cmpc_get_qp_kernel(cmpc_handle h, char *buf, int n) {
     return guard(h, [&] {
         need(buf != nullptr && n > 0, "null output");
         const int P = qp_group(h);
-        const std::string s = P ? "k_qp_group<" + std::to_string(P) + ">"
-                                : "k_qp_ipm<" + std::to_string(qp_waves(h)) + ">";
+        const int tw = qp_split(h);
+        const std::string s = P    ? "k_qp_group<" + std::to_string(P) + ">"
+                              : tw ? "k_qp_ipm<1>+tail<" + std::to_string(tw) + ">"
+                                   : "k_qp_ipm<" + std::to_string(qp_waves(h)) + ">";
         std::snprintf(buf, (size_t)n, "%s", s.c_str());
     });
 }

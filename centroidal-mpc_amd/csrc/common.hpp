@@ -90,6 +90,7 @@ template <typename T> struct DevBuf {
     int32_t *qp_nref;               // (B) refinement steps taken
     int32_t *qp_tail;               // (B) Newton steps run on the whole workgroup after a hand-over (k_qp_group)
     int32_t *qp_polish;             // (B) solution polishing: 1 accepted, -1 rejected, 0 not tried
+    void *qp_state;                 // (B) Newton-loop state of a problem left for the tail launch (split QP)
     // IPM workspace
     T *ws;
     size_t ws_stride;               // elements per problem

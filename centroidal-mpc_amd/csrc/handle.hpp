@@ -56,7 +56,7 @@ struct cmpc_handle_s {
          *Ubar = nullptr, *f = nullptr, *A = nullptr, *Bu = nullptr, *C = nullptr, *K = nullptr, *Sig = nullptr,
          *Acl = nullptr, *Qw = nullptr, *stage = nullptr, *cw = nullptr, *xs = nullptr, *us = nullptr, *ts = nullptr,
          *nus = nullptr, *lams = nullptr, *qp_status = nullptr, *qp_iters = nullptr, *qp_merit = nullptr,
-         *qp_nref = nullptr, *qp_tail = nullptr, *qp_polish = nullptr, *ws = nullptr, *scp = nullptr,
+         *qp_nref = nullptr, *qp_tail = nullptr, *qp_polish = nullptr, *qp_state = nullptr, *qp_split = nullptr, *ws = nullptr, *scp = nullptr,
          *Xacc = nullptr, *Uacc = nullptr, *Kacc = nullptr, *Sacc = nullptr, *stamps = nullptr, *Xlin = nullptr,
          *Ulin = nullptr;
     int scp_mode = CMPC_SCP_MODE_REFERENCE;
@@ -134,7 +134,7 @@ struct cmpc_handle_s {
         d.LS = (size_t)max_batch * N;
         d.xs = (T *)xs; d.us = (T *)us; d.ts = (T *)ts; d.nus = (T *)nus; d.lams = (T *)lams;
         d.qp_status = (int32_t *)qp_status; d.qp_iters = (int32_t *)qp_iters;
-        d.qp_merit = (T *)qp_merit; d.qp_nref = (int32_t *)qp_nref; d.qp_tail = (int32_t *)qp_tail; d.qp_polish = (int32_t *)qp_polish;
+        d.qp_merit = (T *)qp_merit; d.qp_nref = (int32_t *)qp_nref; d.qp_tail = (int32_t *)qp_tail; d.qp_polish = (int32_t *)qp_polish; d.qp_state = qp_state;
         d.ws = (T *)ws; d.ws_stride = ws_stride; d.scp = (cmpc::ScpState *)scp;
         d.Xacc = (T *)Xacc; d.Uacc = (T *)Uacc; d.Kacc = (T *)Kacc; d.Sacc = (T *)Sacc;
         d.stamps = (unsigned long long *)stamps;

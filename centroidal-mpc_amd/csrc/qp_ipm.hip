@@ -459,6 +459,10 @@ __device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<
     const DevParams<T> &P = *C.prm;
     const SV<const T> st{stp};
     const unsigned msk = C.cmask(k);
+    // non-finite detector: the norms are fmax / fmin reductions, which drop NaNs, so every residual
+    // also enters a sum that reaches nm.mu multiplied by zero (NaN or inf there makes mu NaN; the
+    // stopping test and the polished iterate's verification check mu)
+    A nanchk = A(0);
     A x[9], u[NU], x1[9], nk[9], n1[9], w[3];
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
@@ -500,6 +504,7 @@ __device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<
             const A ez = ax[i] + bu[i] - x1[i], r = st[S::R + i];
             const A re = ez - r;
             rde_o[i * ld + 1 + k] = T(re);
+            nanchk += re;
             nm.prim = fmax(nm.prim, T(fabs(re)));
             nm.sp = fmax(nm.sp, T(fmax(fabs(ez), fabs(r))));
         }
@@ -523,6 +528,7 @@ __device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<
     auto row = [&](int r, bool pr, A g, A h) {
         const A v = g - h, sr = ss[r * ld], lr = ls[r * ld];
         rdi_o[r * ld] = pr ? T(v + sr) : T(0);
+        nanchk += pr ? v + sr + lr : A(0);
         const T c = pr ? T(sr * lr) : T(0);
         nm.prim = fmax(nm.prim, pr ? T(v) : T(0));
         nm.sp = fmax(nm.sp, pr ? T(fmax(fabs(g), fabs(g - v))) : T(0));
@@ -578,6 +584,7 @@ __device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<
         const A g = (i >= 6) ? gL[i - 6] : A(0);
         const A rd = hx + q + ex[i] + g;
         rdx_o[i * ld] = T(rd);
+        nanchk += rd;
         nm.dual = fmax(nm.dual, T(fabs(rd)));
         nm.sd = fmax(nm.sd, T(fmax(fabs(hx), fmax(fabs(q), fmax(fabs(ex[i]), fabs(g))))));
     }
@@ -592,10 +599,12 @@ __device__ __forceinline__ void resid_knot(const Ctx<T, ROBOT> &C, int k, Norms<
             const A h = A(C.Wu(i)) * u[i];
             const A rd = h + eu[i] + gu[i];
             rdu_o[i * ld] = T(rd);
+            nanchk += rd;
             nm.dual = fmax(nm.dual, T(fabs(rd)));
             nm.sd = fmax(nm.sd, T(fmax(fabs(h), fmax(fabs(eu[i]), fabs(gu[i])))));
         }
     }
+    nm.mu += T(A(0) * nanchk);
 }
 
 template <typename T, int ROBOT, int PART = -1> __device__ PHASE_ATTR void phase_residual(const Ctx<T, ROBOT> &C, int k, Norms<T, ROBOT> &nm) {
@@ -2315,7 +2324,7 @@ __device__ __forceinline__ void group_done(LdsT<int> *gf, int w) {
 template <typename T, int ROBOT, int G, int WG>
 __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT> &C, int b, IpmState<T> &S,
                                          const IpmLds<T> &L, int max_iter, T eps_abs, T eps_rel, T eta,
-                                         T polish_eps, LdsT<int> *gf = nullptr, int gP = 0) {
+                                         T polish_eps, LdsT<int> *gf = nullptr, int gP = 0, int yield_at = 0) {
     const int tid = threadIdx.x & (G - 1), N = C.N, K1 = N + 1, NB = N + 2, NBm = NB / 2;
     (void)b;
 #ifdef CMPC_STAMPS
@@ -2380,7 +2389,7 @@ __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT>
             T mn[2] = {nm.smin, nm.lmin};
             block_reduce<T, G, 2, 2, WG>(mn, L.red);
             const T mp = fmax(prim / ep, fmax(dual / ed, comp / ec));
-            if (mp <= T(1) && mn[0] >= -ep && mn[1] >= -ed) {
+            if (mp <= T(1) && mn[0] >= -ep && mn[1] >= -ed && mu == mu) {   // (mu: the non-finite detector)
                 merit = mp;
                 status = CMPC_QP_SOLVED;
                 S.polish = 1;
@@ -2434,7 +2443,9 @@ __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT>
         }
         // k_qp_group: every other problem of the workgroup has stopped, so this one continues on
         // all waves from here (the residual pass of this iteration is in the workspace)
-        if (gf && group_handover(gf, gP, (int)(threadIdx.x >> 6), it)) {
+        // split launch (k_qp_ipm MODE 1, head): a problem still running after the stopping test of
+        // iteration yield_at leaves for the tail launch, which resumes it here on all its waves
+        if ((gf && group_handover(gf, gP, (int)(threadIdx.x >> 6), it)) || (yield_at > 0 && it >= yield_at)) {
             S.yielded = 1;
             S.resume = 1;
             S.mu = mu;
@@ -2616,8 +2627,9 @@ __device__ __forceinline__ void ipm_finish(const DevBuf<T> &d, const Ctx<T, ROBO
         for (int i = 0; i < 9; ++i) d.xs[((size_t)b * K1 + k) * 9 + i] = x[i];
         d.ts[(size_t)b * K1 + k] = C.kv(WF(t), k)[0];
         if (k < N) for (int i = 0; i < NU; ++i) d.us[((size_t)b * N + k) * NU + i] = u[i];
+        // (fmax: a polished solution's inactive rows carry multipliers of rounding size, either sign)
         for (int r = 0; r < NI; ++r)
-            d.lams[((size_t)b * K1 + k) * NI + r] = Ctx<T, ROBOT>::present_m(msk, r) ? lm[r] : T(0);
+            d.lams[((size_t)b * K1 + k) * NI + r] = Ctx<T, ROBOT>::present_m(msk, r) ? fmax(lm[r], T(0)) : T(0);
     }
     for (int e = tid; e < NB * 9; e += G) d.nus[(size_t)b * NB * 9 + e] = C.ws[(WF(nu) + e % 9) * KPC + e / 9];
     if (tid == 0) {
@@ -2634,13 +2646,28 @@ __device__ __forceinline__ void ipm_finish(const DevBuf<T> &d, const Ctx<T, ROBO
 }
 
 // One workgroup per problem: one, two or four waves (cmpc_api.cpp qp_waves).
-template <typename T, int ROBOT, int NTT>
+// Split launches (MODE; cmpc_api.cpp qp_split): one wave per problem stops being the batch's
+// bottleneck once its slowest problems are the only ones left.  MODE 1 (head, one wave per
+// problem) lets a problem still running after the stopping test of iteration split[0] leave: its
+// Newton-loop state goes to d.qp_state and its index to the tail list split[2 + i] (count split[1]);
+// MODE 2 (tail, two or four waves per problem) resumes the listed problems there, one per workgroup
+// (workgroups past the count leave at once).  Which problems leave depends on Newton-step counts
+// only, and a resumed problem runs the all-wave algorithm from that iteration, so results are
+// reproducible run to run.  MODE 0: the whole solve.
+template <typename T, int ROBOT, int NTT, int MODE>
 __global__ void __launch_bounds__(NTT, NTT == 128 ? QP_MIN_WAVES_2W : QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int only_active, int max_iter, T eps_abs, T eps_rel,
-                                               T eta, T floor_s, T floor_l, T polish_eps) {
+                                               T eta, T floor_s, T floor_l, T polish_eps, int *split) {
+    static_assert(MODE != 1 || NTT == 64, "the head launch runs one wave per problem");
+    static_assert(MODE != 2 || NTT > 64, "the tail launch runs two or four waves per problem");
     extern __shared__ __attribute__((aligned(16))) unsigned char dsmem[];
-    const int b = blockIdx.x;
-    if (b >= d.B) return;
-    if (only_active && !d.scp[b].active) return;
+    int b = blockIdx.x;
+    if constexpr (MODE == 2) {
+        if (b >= __builtin_amdgcn_readfirstlane(split[1])) return;
+        b = __builtin_amdgcn_readfirstlane(split[2 + b]);
+    } else {
+        if (b >= d.B) return;
+        if (only_active && !d.scp[b].active) return;
+    }
     __shared__ T red[8 * (NTT / 64)];
     __shared__ T sh[NTT >= 256 ? 4 * PT_SCRATCH : 2 * TW_SCRATCH];
     __shared__ T sbv_s[NTT >= 256 ? 6 * 9 : 1];
@@ -2671,9 +2698,26 @@ __global__ void __launch_bounds__(NTT, NTT == 128 ? QP_MIN_WAVES_2W : QP_MIN_WAV
         C.bus = C.hy + vec;
     }
     IpmState<T> S = ipm_state0<T>();
+    if constexpr (MODE == 2) {   // resumed after the head launch's stopping test of iteration S.it
+        S = reinterpret_cast<const IpmState<T> *>(d.qp_state)[b];
+        S.yielded = 0;
+        const int it0 = S.it;
+        ipm_loop<T, ROBOT, NTT, NTT>(d, C, b, S, L, max_iter, eps_abs, eps_rel, eta, polish_eps);
+        S.tail = S.it - it0;
+        ipm_finish<T, ROBOT, NTT>(d, C, b, S);
+        return;
+    }
     ipm_start<T, ROBOT, NTT, NTT>(d, C, b);
-    ipm_loop<T, ROBOT, NTT, NTT>(d, C, b, S, L, max_iter, eps_abs, eps_rel, eta, polish_eps);
-    ipm_finish<T, ROBOT, NTT>(d, C, b, S);
+    const int yield_at = MODE == 1 ? __builtin_amdgcn_readfirstlane(split[0]) : 0;
+    ipm_loop<T, ROBOT, NTT, NTT>(d, C, b, S, L, max_iter, eps_abs, eps_rel, eta, polish_eps, nullptr, 0, yield_at);
+    if (MODE == 1 && S.yielded) {
+        if (tid == 0) {
+            reinterpret_cast<IpmState<T> *>(d.qp_state)[b] = S;
+            split[2 + atomicAdd(split + 1, 1)] = b;
+        }
+    } else {
+        ipm_finish<T, ROBOT, NTT>(d, C, b, S);
+    }
     // Covariance scans of a deterministic batch (cmpc_api.cpp launch_phase): a workgroup whose QP
     // has finished takes scan jobs from the counter until none is left, so the scans fill the
     // SIMDs of problems that converged early.  Every workgroup leaves after one failed take.  Only
@@ -2692,6 +2736,34 @@ __global__ void __launch_bounds__(NTT, NTT == 128 ? QP_MIN_WAVES_2W : QP_MIN_WAV
             if (only_active && !d.scp[j].active) continue;
             if (tid < 64) cov_scan_problem<T, ROBOT>(d, j, scan_lds);
         }
+    }
+}
+
+// Yield iteration of a split launch (MODE 1): the smallest K >= 2 such that at most `cap`
+// problems took more than K Newton-loop iterations in the previous QP launch (so the tail launch
+// runs in one round, a problem per CU); 0 (no split) for a batch never solved (its counts are
+// cleared by the upload) or when no such K below the cap exists.  split[1] (the tail count) reset.
+// One workgroup of 1024 threads.
+template <typename T> __global__ void __launch_bounds__(1024) k_qp_split(DevBuf<T> d, int only_active, int cap, int *split) {
+    __shared__ int hist[64];
+    if (threadIdx.x < 64) hist[threadIdx.x] = 0;
+    __syncthreads();
+    for (int b = threadIdx.x; b < d.B; b += 1024) {
+        const int it = (only_active && !d.scp[b].active) ? 0 : d.qp_iters[b];
+        atomicAdd(&hist[it < 0 ? 0 : (it > 63 ? 63 : it)], 1);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int K = 0, above = 0, any = 0;
+        for (int k = 63; k >= 1; --k) any += hist[k];
+        if (any > 0)
+            for (int k = 63; k >= 2; --k) {   // above = #(iterations > k - 1) as k decreases
+                if (above + hist[k] > cap) { K = k; break; }
+                above += hist[k];
+            }
+        // K: the largest count whose inclusion would exceed the cap, so #(iterations > K) <= cap
+        split[0] = K;
+        split[1] = 0;
     }
 }
 
@@ -2898,9 +2970,9 @@ template <typename T> __global__ void __launch_bounds__(1024) k_qp_order(DevBuf<
 }
 
 #define INST(T, R)                                                                       \
-    template __global__ void k_qp_ipm<T, R, 64>(DevBuf<T>, int, int, T, T, T, T, T, T);     \
-    template __global__ void k_qp_ipm<T, R, 128>(DevBuf<T>, int, int, T, T, T, T, T, T);    \
-    template __global__ void k_qp_ipm<T, R, 256>(DevBuf<T>, int, int, T, T, T, T, T, T);    \
+    template __global__ void k_qp_ipm<T, R, 64, 0>(DevBuf<T>, int, int, T, T, T, T, T, T, int *);     \
+    template __global__ void k_qp_ipm<T, R, 128, 0>(DevBuf<T>, int, int, T, T, T, T, T, T, int *);    \
+    template __global__ void k_qp_ipm<T, R, 256, 0>(DevBuf<T>, int, int, T, T, T, T, T, T, int *);    \
     template __global__ void k_qp_group<T, R, 2>(DevBuf<T>, const int *, int, int, int, T, T, T, T, T, T); \
     template __global__ void k_qp_group<T, R, 4>(DevBuf<T>, const int *, int, int, int, T, T, T, T, T, T);
 INST(double, 0)
@@ -2908,6 +2980,14 @@ INST(double, 1)
 INST(float, 0)
 INST(float, 1)
 #undef INST
+// split launches: fp64 only (fp32 batches take two Newton steps, no tail to split off)
+template __global__ void k_qp_ipm<double, 0, 64, 1>(DevBuf<double>, int, int, double, double, double, double, double, double, int *);
+template __global__ void k_qp_ipm<double, 1, 64, 1>(DevBuf<double>, int, int, double, double, double, double, double, double, int *);
+template __global__ void k_qp_ipm<double, 0, 128, 2>(DevBuf<double>, int, int, double, double, double, double, double, double, int *);
+template __global__ void k_qp_ipm<double, 1, 128, 2>(DevBuf<double>, int, int, double, double, double, double, double, double, int *);
+template __global__ void k_qp_ipm<double, 0, 256, 2>(DevBuf<double>, int, int, double, double, double, double, double, double, int *);
+template __global__ void k_qp_ipm<double, 1, 256, 2>(DevBuf<double>, int, int, double, double, double, double, double, double, int *);
+template __global__ void k_qp_split<double>(DevBuf<double>, int, int, int *);
 template __global__ void k_qp_order<double>(DevBuf<double>, int, int, int *);
 template __global__ void k_qp_order<float>(DevBuf<float>, int, int, int *);
 
@@ -2926,6 +3006,8 @@ size_t ipm_lds_bytes(int N, int prec_bytes, int nt) {
     const size_t nring = nt >= 256 ? 4 : 2;
     return std::max<size_t>(vec + nring * SWEEP_LDS + (nt > 64 ? vec : 0) + (nt >= 256 ? 2 * vec : 0), SCAN_LDS) * prec_bytes;
 }
+
+size_t ipm_state_bytes(int prec_bytes) { return prec_bytes == 8 ? sizeof(IpmState<double>) : sizeof(IpmState<float>); }
 
 size_t ipm_workspace_elems(int N, int robot) {
     (void)N;

@@ -99,7 +99,8 @@ def robot_defaults(qp):
 
 def solve(qp, eps=1e-11, max_iter=60, eta=0.999, verbose=False, reg=0.0, piv_floor=1e-13, dcap_rel=1e12,
           refine_alpha=0.5, refine_merit=1e6, eps_pinf=1e-4, init_floor=INIT_FLOOR,
-          init_floor_l=INIT_FLOOR_L, fric_floor=1e-9, polish=False, polish_eps=None, polish_rel=1e-14):
+          init_floor_l=INIT_FLOOR_L, fric_floor=1e-9, polish=False, polish_eps=None, polish_rel=1e-14,
+          comp_primal=None):
     if polish_eps is None:
         polish_eps = eps
     N, nc, nu, nupc = qp.N, qp.nc, qp.nu, qp.nupc
@@ -211,7 +212,7 @@ def solve(qp, eps=1e-11, max_iter=60, eta=0.999, verbose=False, reg=0.0, piv_flo
                       np.abs(qp.Wu * u).max(), np.abs(eu).max(), np.abs(gu).max(), 1.0)
         # complementarity against the primal scale on Solo12, the dual scale on TALOS (qp_ipm.hip
         # COMP_PRIMAL_SCALE)
-        scale_c = scale_d if talos else scale_p
+        scale_c = scale_p if (comp_primal if comp_primal is not None else not talos) else scale_d
         hist.append((it, prim, dual, comp, mu_))
         if verbose:
             print('it %2d prim %.2e dual %.2e comp %.2e mu %.2e' % (it, prim, dual, comp, mu_))
