@@ -2388,8 +2388,11 @@ __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT>
         if (pm == 2) {   // the polished iterate: an exact KKT point within eps, or back to the old one
             T mn[2] = {nm.smin, nm.lmin};
             block_reduce<T, G, 2, 2, WG>(mn, L.red);
-            const T mp = fmax(prim / ep, fmax(dual / ed, comp / ec));
-            if (mp <= T(1) && mn[0] >= -ep && mn[1] >= -ed && mu == mu) {   // (mu: the non-finite detector)
+            // primal side 100x tighter than the stopping test: the interior-point iterates satisfy
+            // their rows to rounding, and a polished point must not trade that for its active set
+            // (a TALOS N=50 polish verified at eps left a 1.7e-8 row violation)
+            const T mp = fmax(prim / (T(0.01) * ep), fmax(dual / ed, comp / ec));
+            if (mp <= T(1) && mn[0] >= -T(0.01) * ep && mn[1] >= -ed && mu == mu) {   // (mu: the non-finite detector)
                 merit = mp;
                 status = CMPC_QP_SOLVED;
                 S.polish = 1;

@@ -495,7 +495,9 @@ def _polish(qp, masks, x, u, t, nu_, s, lam, last, system, GT, ET, Ez, ineq_val,
     lmin = min(float(np.min(np.where(ac, li, np.inf))) for li, ac in zip(l2, act))
     smin = min(float(np.min(np.where((mk > 0) & ~ac, -v, np.inf)))
                for v, ac, mk in zip(ineq_val(x2, u2, t2), act, masks))
-    ok = lmin >= -eps * scale_d and smin >= -eps * scale_p
+    prim2 = np.abs(Ez(x2, u2) - e_rhs).max()
+    # as the kernel (ipm_loop, pm == 2): the primal side 100x tighter than the stopping test
+    ok = lmin >= -eps * scale_d and smin >= -0.01 * eps * scale_p and prim2 <= 0.01 * eps * scale_p and np.isfinite(x2).all()
     return dict(status=1 if ok else -1, x=x2, u=u2, t=t2, nu=n2, s=s2, lam=l2, lmin=lmin, smin=smin,
                 n_active=int(sum(a_.sum() for a_ in act)))
 

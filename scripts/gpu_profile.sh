@@ -16,7 +16,7 @@ export CMPC_HEAD=${CMPC_HEAD:-?}
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { cat gpurun_out/smoke.log; exit 1; }
 tail -1 gpurun_out/smoke.log
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o trace -- \
-    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-extras > gpurun_out/prof_bench_$TAG.log 2>&1 || { tail -20 gpurun_out/prof_bench_$TAG.log; exit 1; }
+    python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extras > gpurun_out/prof_bench_$TAG.log 2>&1 || { tail -20 gpurun_out/prof_bench_$TAG.log; exit 1; }
 tail -1 gpurun_out/prof_bench_$TAG.log
 pmc() {   # pmc <name> <counters> <bench args>
     local name=$1 ctr=$2; shift 2
