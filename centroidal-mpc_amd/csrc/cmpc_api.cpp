@@ -174,9 +174,11 @@ int qp_pair_share() {
 // previous launch's Newton counts).  Round 4's replacement for the grouped kernel (qp_group).
 // CMPC_QP_SPLIT=0 turns it off.  Returns the tail launch's waves per problem, or 0.
 int qp_split(cmpc_handle h) {
-    if (h->prec != CMPC_PREC_F64 || qp_waves(h) != 1 || h->B <= h->n_cu || qp_group(h)) return 0;
+    const int w = qp_waves(h);
+    if (h->prec != CMPC_PREC_F64 || w > 2 || h->B <= h->n_cu || qp_group(h)) return 0;
     if (const char *e = std::getenv("CMPC_QP_SPLIT"))
         if (e[0] == '0') return 0;
+    if (w == 2 && h->N < 40) return 0;   // (a two-wave head needs the four-wave tail)
     return h->N >= 40 ? 4 : 2;
 }
 
@@ -198,17 +200,18 @@ double qp_eps_default(cmpc_handle h) {
 double qp_eps_abs(cmpc_handle h) { return h->qs.eps_abs > 0 ? h->qs.eps_abs : qp_eps_default(h); }
 double qp_eps_rel(cmpc_handle h) { return h->qs.eps_rel > 0 ? h->qs.eps_rel : qp_eps_default(h); }
 
-// Polishing tolerance: the setting, or (< 0) the robot's.  Solo12 polishes at 1e-8 (10x its eps):
-// on the GPU at the metric config the guess from 1e-9 was right on 296 problems and wrong on 4,
-// the slowest ones, where a rejected polish only adds a step (gpurun_out r04e, DESIGN.md
-// "Polishing"); TALOS N=200 at 1e-7 (15.4 -> 13.0 Newton steps on C4, 499 of 512 accepted).
+// Polishing tolerance: the setting, or (< 0) the robot's.  Same-box sweeps (profiles/r04a_polish_sweep.log):
+// Solo12 trot N=100 x 1024 polishes at 1e-7 on 820 of 1024 problems (1 wrong guess), 4.67 Newton
+// steps against 5.48 without, 281.8k SCP it/s against 276.8k (1e-8: 273.0k).  TALOS (BASELINE C4
+// from its fourth SCP iteration) guesses wrong on 384 of 512 at 1e-7 and 99-166 at 1e-8 / 1e-9, where
+// every rejected polish costs a factorization: 51.7k against 54.3k without, so TALOS does not polish.
 // fp32 (C3) is not polished.
 double qp_polish_eps(cmpc_handle h) {
     if (h->prec != CMPC_PREC_F64) return 0.0;
     if (const char *e = std::getenv("CMPC_QP_POLISH_EPS"))   // diagnostic override (A/B runs)
         return std::atof(e);
     if (h->qs.polish_eps >= 0) return h->qs.polish_eps;
-    return h->robot == 1 ? 1e-7 : 1e-8;
+    return h->robot == 1 ? 0.0 : 1e-7;
 }
 
 // Covariance scan placement.  Sigma feeds only the chance-constraint back-off of stochastic
@@ -349,8 +352,15 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
             if (tw) {   // split launches: head (one wave per problem, the slowest leave), tail
                 int *sp = (int *)h->qp_split;
                 hipLaunchKernelGGL((k_qp_split<T>), dim3(1), dim3(1024), 0, h->stream, d, only_active, h->n_cu, sp);
-                hipLaunchKernelGGL((k_qp_ipm<T, R, 64, 1>), dim3(B), dim3(64), lds, h->stream, d, only_active,
-                                   h->qs.max_iter, ea, er, eta, fs, fl, pe, sp);
+                if (nt == 128) {   // two-wave head (BASELINE C4: TALOS N=200 x 512)
+                    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_qp_ipm<T, R, 128, 1>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                    hipLaunchKernelGGL((k_qp_ipm<T, R, 128, 1>), dim3(B), dim3(128), lds, h->stream, d, only_active,
+                                       h->qs.max_iter, ea, er, eta, fs, fl, pe, sp);
+                } else {
+                    hipLaunchKernelGGL((k_qp_ipm<T, R, 64, 1>), dim3(B), dim3(64), lds, h->stream, d, only_active,
+                                       h->qs.max_iter, ea, er, eta, fs, fl, pe, sp);
+                }
                 DevBuf<T> dt = d;
                 dt.scan_ctr = nullptr;
                 const size_t lt = ipm_lds_bytes(h->N, (int)sizeof(T), 64 * tw);
@@ -1501,7 +1511,7 @@ int cmpc_get_qp_kernel(cmpc_handle h, char *buf, int n) {
         const int P = qp_group(h);
         const int tw = qp_split(h);
         const std::string s = P    ? "k_qp_group<" + std::to_string(P) + ">"
-                              : tw ? "k_qp_ipm<1>+tail<" + std::to_string(tw) + ">"
+                              : tw ? "k_qp_ipm<" + std::to_string(qp_waves(h)) + ">+tail<" + std::to_string(tw) + ">"
                                    : "k_qp_ipm<" + std::to_string(qp_waves(h)) + ">";
         std::snprintf(buf, (size_t)n, "%s", s.c_str());
     });

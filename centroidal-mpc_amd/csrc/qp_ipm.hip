@@ -2649,9 +2649,9 @@ __device__ __forceinline__ void ipm_finish(const DevBuf<T> &d, const Ctx<T, ROBO
 }
 
 // One workgroup per problem: one, two or four waves (cmpc_api.cpp qp_waves).
-// Split launches (MODE; cmpc_api.cpp qp_split): one wave per problem stops being the batch's
-// bottleneck once its slowest problems are the only ones left.  MODE 1 (head, one wave per
-// problem) lets a problem still running after the stopping test of iteration split[0] leave: its
+// Split launches (MODE; cmpc_api.cpp qp_split): a launch of one (two) waves per problem that fills
+// the device lasts as long as its slowest problems.  MODE 1 (head, one or two waves per problem)
+// lets a problem still running after the stopping test of iteration split[0] leave: its
 // Newton-loop state goes to d.qp_state and its index to the tail list split[2 + i] (count split[1]);
 // MODE 2 (tail, two or four waves per problem) resumes the listed problems there, one per workgroup
 // (workgroups past the count leave at once).  Which problems leave depends on Newton-step counts
@@ -2660,7 +2660,7 @@ __device__ __forceinline__ void ipm_finish(const DevBuf<T> &d, const Ctx<T, ROBO
 template <typename T, int ROBOT, int NTT, int MODE>
 __global__ void __launch_bounds__(NTT, NTT == 128 ? QP_MIN_WAVES_2W : QP_MIN_WAVES) k_qp_ipm(DevBuf<T> d, int only_active, int max_iter, T eps_abs, T eps_rel,
                                                T eta, T floor_s, T floor_l, T polish_eps, int *split) {
-    static_assert(MODE != 1 || NTT == 64, "the head launch runs one wave per problem");
+    static_assert(MODE != 1 || NTT <= 128, "the head launch runs one or two waves per problem");
     static_assert(MODE != 2 || NTT > 64, "the tail launch runs two or four waves per problem");
     extern __shared__ __attribute__((aligned(16))) unsigned char dsmem[];
     int b = blockIdx.x;
@@ -2986,6 +2986,8 @@ INST(float, 1)
 // split launches: fp64 only (fp32 batches take two Newton steps, no tail to split off)
 template __global__ void k_qp_ipm<double, 0, 64, 1>(DevBuf<double>, int, int, double, double, double, double, double, double, int *);
 template __global__ void k_qp_ipm<double, 1, 64, 1>(DevBuf<double>, int, int, double, double, double, double, double, double, int *);
+template __global__ void k_qp_ipm<double, 0, 128, 1>(DevBuf<double>, int, int, double, double, double, double, double, double, int *);
+template __global__ void k_qp_ipm<double, 1, 128, 1>(DevBuf<double>, int, int, double, double, double, double, double, double, int *);
 template __global__ void k_qp_ipm<double, 0, 128, 2>(DevBuf<double>, int, int, double, double, double, double, double, double, int *);
 template __global__ void k_qp_ipm<double, 1, 128, 2>(DevBuf<double>, int, int, double, double, double, double, double, double, int *);
 template __global__ void k_qp_ipm<double, 0, 256, 2>(DevBuf<double>, int, int, double, double, double, double, double, double, int *);

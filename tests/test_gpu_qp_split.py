@@ -8,7 +8,7 @@ above it in the previous launch's Newton counts; no split on a batch's first lau
 in the workspace, and the tail launch resumes it on four waves (two below N = 40), where the Schur
 recurrence runs as four chains (a different elimination order) or two ends.  So: statuses and SCP
 decisions agree, Newton counts within one, solutions to 1e-7 relative (TALOS: counts within 2,
-solutions within the oracle parity bar 1e-5), on the fixed-K path and the early-exit path (solve_scp,
+solutions within the oracle parity bar 1e-5), with one- and two-wave heads, on the fixed-K path and the early-exit path (solve_scp,
 only active problems); and two runs are bit-identical (the yield point depends on Newton counts only).
 """
 import os
@@ -37,10 +37,10 @@ class _split:
             os.environ['CMPC_QP_SPLIT'] = self.old
 
 
-def _run(pb, on, steps=3):
+def _run(pb, on, steps=3, waves=1):
     with _split(on):
         s = Solver(pb.robot, pb.N, pb.B, 'fp64')
-        s.set_qp_settings(waves_per_problem=1)
+        s.set_qp_settings(waves_per_problem=waves)
         s.upload(pb)
         kernel = s.qp_kernel()
         out = []
@@ -52,16 +52,17 @@ def _run(pb, on, steps=3):
     return kernel, out
 
 
-CASES = [('trot', 100, 320), ('trot', 30, 300), ('pace', 60, 300), ('bound', 60, 300), ('talos', 40, 300)]
+CASES = [('trot', 100, 320, 1), ('trot', 30, 300, 1), ('pace', 60, 300, 1), ('bound', 60, 300, 1), ('talos', 40, 300, 1),
+         ('trot', 100, 320, 2), ('talos', 80, 300, 2)]   # (two-wave heads: BASELINE C4's shape)
 
 
-@pytest.mark.parametrize('cfg,N,B', CASES)
-def test_split_launches_match_one_launch(cfg, N, B):
+@pytest.mark.parametrize('cfg,N,B,waves', CASES)
+def test_split_launches_match_one_launch(cfg, N, B, waves):
     pb = make_batch(cfg, N, B, seed_offset=71)
-    k1, one = _run(pb, False)
-    k2, spl = _run(pb, True)
-    assert k1 == 'k_qp_ipm<1>', k1
-    assert k2 == 'k_qp_ipm<1>+tail<%d>' % (4 if N >= 40 else 2), k2
+    k1, one = _run(pb, False, waves=waves)
+    k2, spl = _run(pb, True, waves=waves)
+    assert k1 == 'k_qp_ipm<%d>' % waves, k1
+    assert k2 == 'k_qp_ipm<%d>+tail<%d>' % (waves, 4 if N >= 40 else 2), k2
     talos = cfg == 'talos'
     tails = 0
     for (z1, s1, i1, d1, t1), (z2, s2, i2, d2, t2) in zip(one, spl):

@@ -119,13 +119,15 @@ def _scp0(cfg, N, b):
 @pytest.mark.parametrize('cfg,N,b', [('talos', 40, 5), ('talos', 40, 4), ('trot', 40, 2), ('trot', 40, 9)])
 def test_polish_reaches_the_exact_minimizer(cfg, N, b):
     """Solution polishing (the reference runs OSQP with polish=True, src/scp_solver.py:62), at the
-    kernel's robot defaults (Solo12 eps 1e-9, polish 1e-8; TALOS 1e-10, 1e-7): once the iterate
+    kernel's robot defaults (Solo12 eps 1e-9, polish 1e-7; TALOS eps 1e-10, polish 1e-7 here, off in
+    the kernel by default): once the iterate
     meets polish_eps, the active set guessed from the last step (Tapia indicators) gives a reduced
     KKT system; its solution, verified at eps, is the QP's exact minimizer (<= 1e-8 of an
     independent sparse IPM run to 1e-12, and no farther than the unpolished solve) in fewer Newton
     steps than the unpolished solve."""
     qp, ref_qp = _scp0(cfg, N, b)
     eps, peps = IM.robot_defaults(qp)
+    peps = peps or 1e-7   # (TALOS does not polish by default; the algorithm is checked at 1e-7)
     plain = IM.solve(qp, eps=eps)
     pol = IM.solve(qp, eps=eps, polish=True, polish_eps=peps)
     assert plain['status'] == 1 and pol['status'] == 1
@@ -139,11 +141,12 @@ def test_polish_reaches_the_exact_minimizer(cfg, N, b):
 
 
 def test_rejected_polish_rolls_back():
-    """A wrong active-set guess (TALOS problem 8 at its defaults): the verification fails, the
+    """A wrong active-set guess (TALOS problem 8 at polish_eps 1e-9): the verification fails, the
     iterate before the polish is restored and the interior-point iterations finish exactly as
     without polishing."""
     qp, _ = _scp0('talos', 40, 8)
-    eps, peps = IM.robot_defaults(qp)
+    eps, _ = IM.robot_defaults(qp)
+    peps = 1e-9
     plain = IM.solve(qp, eps=eps)
     pol = IM.solve(qp, eps=eps, polish=True, polish_eps=peps)
     assert [p['status'] for p in pol['polish_log']] == [-1] and pol['status'] == 1
