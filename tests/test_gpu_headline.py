@@ -20,7 +20,7 @@ The trot QPs are nearly flat along some contact-force directions (curvature 1 ag
 two solutions differ by more than 1e-5, the GPU's must be feasible to 1e-8 and its objective no
 higher than the oracle's by more than 1e-12 of it (problem 170 of the metric batch: the GPU's point is
 the lower one).
-The same on the 2-GPU shard of the metric (512 problems: k_qp_ipm<2>, two waves per problem) and the
+The same on the 2-GPU shard of the metric (512 problems: a two-wave head k_qp_ipm<2> + the tail) and the
 4-GPU shard (256 problems: k_qp_ipm<4>, four chains).
 """
 import numpy as np
@@ -97,7 +97,7 @@ def test_metric_config_kernel_matches_oracle():
         s.close()
 
 
-@pytest.mark.parametrize('B,kernel', [(512, 'k_qp_ipm<2>'), (256, 'k_qp_ipm<4>')])
+@pytest.mark.parametrize('B,kernel', [(512, 'k_qp_ipm<2>+tail<4>'), (256, 'k_qp_ipm<4>')])
 def test_metric_shards_match_oracle(B, kernel):
     """The 2- and 4-GPU slices of the metric's 1024 problems (cmpc/shard.py: contiguous slices)."""
     s, k, z, y, st, it = _sorted_launch(B, seed_offset=0)
