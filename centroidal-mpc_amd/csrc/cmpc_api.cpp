@@ -22,7 +22,7 @@ template <typename T, int R> __global__ void k_lin_knots(DevBuf<T>, int, int);
 template <typename T, int R> __global__ void k_cov_scan(DevBuf<T>, int);
 template <typename T, int R, bool FULL> __global__ void k_assemble(DevBuf<T>, int);
 template <typename T, int R, int NTT, int MODE> __global__ void k_qp_ipm(DevBuf<T>, int, int, T, T, T, T, T, T, int *);
-template <typename T> __global__ void k_qp_split(DevBuf<T>, int, int, int *);
+template <typename T> __global__ void k_qp_split(DevBuf<T>, int, int, int, int *);
 size_t ipm_state_bytes(int prec_bytes);
 template <typename T, int R, int P> __global__ void k_qp_group(DevBuf<T>, const int *, int, int, int, T, T, T, T, T, T);
 template <typename T> __global__ void k_qp_order(DevBuf<T>, int, int, int *);
@@ -182,6 +182,17 @@ int qp_split(cmpc_handle h) {
     return h->N >= 40 ? 4 : 2;
 }
 
+// Yield iteration of a split launch on a never-solved batch (the reference's use: every solve_scp
+// call is a new problem, src/scp_solver.py:118-179), where there are no Newton counts to pick it
+// from: the robot's prior, above its typical counts so that few problems exceed it (Solo12 trot
+// N=100: 4-8 steps, 6 leaves ~10% for the tail; TALOS N=200: 12-17, 15).  CMPC_QP_SPLIT_FRESH=0
+// turns it off (the first launch is then unsplit).
+int qp_split_prior(cmpc_handle h) {
+    if (const char *e = std::getenv("CMPC_QP_SPLIT_FRESH"))
+        if (e[0] == '0') return 0;
+    return h->robot == 1 ? 15 : 6;
+}
+
 // QP step fraction: the setting, or (0) the robot's. Same-box A/B, bench lines A B A B:
 // Solo12 trot N=100 x 1024 0.995 -> 0.999 316.8k -> 319.5k SCP it/s, 4.81 -> 4.67 Newton steps
 // (profiles/r02_eta999_ab.jsonl); TALOS N=200 x 512 0.999 -> 0.995 56.2k -> 59.4k
@@ -197,8 +208,18 @@ double qp_eps_default(cmpc_handle h) {
     if (h->prec != CMPC_PREC_F64) return 1e-6;
     return h->robot == 1 ? 1e-10 : 1e-9;
 }
-double qp_eps_abs(cmpc_handle h) { return h->qs.eps_abs > 0 ? h->qs.eps_abs : qp_eps_default(h); }
-double qp_eps_rel(cmpc_handle h) { return h->qs.eps_rel > 0 ? h->qs.eps_rel : qp_eps_default(h); }
+double qp_eps_env() {   // CMPC_QP_EPS: diagnostic override of both tolerances (A/B runs)
+    const char *e = std::getenv("CMPC_QP_EPS");
+    return e ? std::atof(e) : 0.0;
+}
+double qp_eps_abs(cmpc_handle h) {
+    if (qp_eps_env() > 0) return qp_eps_env();
+    return h->qs.eps_abs > 0 ? h->qs.eps_abs : qp_eps_default(h);
+}
+double qp_eps_rel(cmpc_handle h) {
+    if (qp_eps_env() > 0) return qp_eps_env();
+    return h->qs.eps_rel > 0 ? h->qs.eps_rel : qp_eps_default(h);
+}
 
 // Polishing tolerance: the setting, or (< 0) the robot's.  Same-box sweeps (profiles/r04a_polish_sweep.log):
 // Solo12 trot N=100 x 1024 polishes at 1e-7 on 820 of 1024 problems (1 wrong guess), 4.67 Newton
@@ -351,7 +372,8 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
         if constexpr (sizeof(T) == 8) {
             if (tw) {   // split launches: head (one wave per problem, the slowest leave), tail
                 int *sp = (int *)h->qp_split;
-                hipLaunchKernelGGL((k_qp_split<T>), dim3(1), dim3(1024), 0, h->stream, d, only_active, h->n_cu, sp);
+                hipLaunchKernelGGL((k_qp_split<T>), dim3(1), dim3(1024), 0, h->stream, d, only_active, h->n_cu,
+                                   qp_split_prior(h), sp);
                 if (nt == 128) {   // two-wave head (BASELINE C4: TALOS N=200 x 512)
                     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_qp_ipm<T, R, 128, 1>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

@@ -32,6 +32,8 @@
 // first refinement; inlined, no flat instruction is left).  CMPC_NOINLINE (diagnostic builds) outlines them.
 #ifdef CMPC_NOINLINE
 #define PHASE_ATTR __attribute__((noinline))
+#elif defined(CMPC_PHASE_FREE)   // diagnostic builds: the compiler's own inlining decisions
+#define PHASE_ATTR
 #else
 #define PHASE_ATTR __attribute__((always_inline))
 #endif
@@ -2184,8 +2186,13 @@ template <int G> constexpr bool split_knots() { return G >= 256; }
 // one friction row at s lambda ~ 5e-6 and solutions up to 7e-5 away from the exact minimizer (the
 // round-4 headline check); with the primal scale at eps 1e-9 every one of 64 problems sampled lands
 // within 4e-7, at 5.1 Newton steps against 4.6 (oracle/ipm_mirror.py, DESIGN.md "Stopping test").
-// TALOS keeps the dual scale (within 9e-7 already; the primal scale cost it 1.3 steps).
+// TALOS keeps the dual scale (within 9e-7 already; the primal scale cost it 1.3 steps), and so does
+// fp32 (eps 1e-6: BASELINE C3 took 4 Newton steps instead of 2 with the primal scale, round 4).
+#ifdef CMPC_COMP_DUAL   // diagnostic builds: round 3's test (the dual scale) for every robot
+template <int ROBOT> __device__ __forceinline__ constexpr bool COMP_PRIMAL_SCALE() { return false; }
+#else
 template <int ROBOT> __device__ __forceinline__ constexpr bool COMP_PRIMAL_SCALE() { return ROBOT == 0; }
+#endif
 
 // Newton-loop state of one problem's solve (carried across k_qp_group's change of mode).  A solve
 // handed over after the stopping test of iteration `it` (yielded) resumes there on all waves: the
@@ -2383,7 +2390,7 @@ __device__ __forceinline__ void ipm_loop(const DevBuf<T> &d, const Ctx<T, ROBOT>
         cnt = sm2[1];
         // complementarity is measured against the primal scale on Solo12 and against the dual scale
         // on TALOS (COMP_PRIMAL_SCALE)
-        const T sc = COMP_PRIMAL_SCALE<ROBOT>() ? sp : sdd;
+        const T sc = (COMP_PRIMAL_SCALE<ROBOT>() && sizeof(T) == 8) ? sp : sdd;
         const T ep = eps_abs + eps_rel * sp, ed = eps_abs + eps_rel * sdd, ec = eps_abs + eps_rel * sc;
         if (pm == 2) {   // the polished iterate: an exact KKT point within eps, or back to the old one
             T mn[2] = {nm.smin, nm.lmin};
@@ -2744,10 +2751,10 @@ __global__ void __launch_bounds__(NTT, NTT == 128 ? QP_MIN_WAVES_2W : QP_MIN_WAV
 
 // Yield iteration of a split launch (MODE 1): the smallest K >= 2 such that at most `cap`
 // problems took more than K Newton-loop iterations in the previous QP launch (so the tail launch
-// runs in one round, a problem per CU); 0 (no split) for a batch never solved (its counts are
-// cleared by the upload) or when no such K below the cap exists.  split[1] (the tail count) reset.
+// runs in one round, a problem per CU); for a batch never solved (its counts are cleared by the
+// upload) the prior k_fresh; 0 (no split) when no such K exists.  split[1] (the tail count) reset.
 // One workgroup of 1024 threads.
-template <typename T> __global__ void __launch_bounds__(1024) k_qp_split(DevBuf<T> d, int only_active, int cap, int *split) {
+template <typename T> __global__ void __launch_bounds__(1024) k_qp_split(DevBuf<T> d, int only_active, int cap, int k_fresh, int *split) {
     __shared__ int hist[64];
     if (threadIdx.x < 64) hist[threadIdx.x] = 0;
     __syncthreads();
@@ -2759,7 +2766,8 @@ template <typename T> __global__ void __launch_bounds__(1024) k_qp_split(DevBuf<
     if (threadIdx.x == 0) {
         int K = 0, above = 0, any = 0;
         for (int k = 63; k >= 1; --k) any += hist[k];
-        if (any > 0)
+        if (any == 0) K = k_fresh;   // a batch never solved: the robot's prior (cmpc_api.cpp qp_split_prior)
+        else
             for (int k = 63; k >= 2; --k) {   // above = #(iterations > k - 1) as k decreases
                 if (above + hist[k] > cap) { K = k; break; }
                 above += hist[k];
@@ -2992,7 +3000,7 @@ template __global__ void k_qp_ipm<double, 0, 128, 2>(DevBuf<double>, int, int, d
 template __global__ void k_qp_ipm<double, 1, 128, 2>(DevBuf<double>, int, int, double, double, double, double, double, double, int *);
 template __global__ void k_qp_ipm<double, 0, 256, 2>(DevBuf<double>, int, int, double, double, double, double, double, double, int *);
 template __global__ void k_qp_ipm<double, 1, 256, 2>(DevBuf<double>, int, int, double, double, double, double, double, double, int *);
-template __global__ void k_qp_split<double>(DevBuf<double>, int, int, int *);
+template __global__ void k_qp_split<double>(DevBuf<double>, int, int, int, int *);
 template __global__ void k_qp_order<double>(DevBuf<double>, int, int, int *);
 template __global__ void k_qp_order<float>(DevBuf<float>, int, int, int *);
 

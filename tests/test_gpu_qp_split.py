@@ -4,7 +4,8 @@ problems to the same answers as one launch of one wave per problem.
 Batches of one wave per problem that fill the device (more problems than CUs) last as long as their
 slowest problems.  The head launch runs every problem on one wave; a problem still running after the
 stopping test of the yield iteration K (k_qp_split: the smallest K with at most one problem per CU
-above it in the previous launch's Newton counts; no split on a batch's first launch) leaves its state
+above it in the previous launch's Newton counts; on a batch's first launch the robot's prior, 6 on
+Solo12) leaves its state
 in the workspace, and the tail launch resumes it on four waves (two below N = 40), where the Schur
 recurrence runs as four chains (a different elimination order) or two ends.  So: statuses and SCP
 decisions agree, Newton counts within one, solutions to 1e-7 relative (TALOS: counts within 2,
@@ -73,7 +74,6 @@ def test_split_launches_match_one_launch(cfg, N, B, waves):
         assert err.max() <= (1e-5 if talos else 1e-7), err.max()
         assert np.all(t1 == 0)
         tails += int((t2 > 0).sum())
-    assert np.all(spl[0][4] == 0)   # the batch's first launch has no counts to split by
     # a tail exists once the counts differ (bound: every problem takes the same number of steps)
     spread = any(o[2].max() > o[2].min() for o in one[:-1])
     assert (tails > 0) == spread, (tails, [np.unique(o[2]) for o in one])
@@ -111,3 +111,30 @@ def test_split_early_exit_path(cfg, N, B):
         assert err <= tol, (k, err)
     np.testing.assert_array_equal(ha[1], hb[1])
     np.testing.assert_array_equal(ha[0]['decision'], hb[0]['decision'])
+
+
+def test_split_on_a_fresh_batch_uses_the_prior():
+    """A never-solved batch has no Newton counts: its first launch yields at the robot's prior
+    (cmpc_api.cpp qp_split_prior, 6 on Solo12), so exactly the problems that need more than 6
+    Newton-loop iterations finish in the tail; with the prior off (CMPC_QP_SPLIT_FRESH=0) the first
+    launch is unsplit.  Both agree with one launch to 1e-7."""
+    pb = make_batch('trot', 100, 320, seed_offset=83)
+    _, one = _run(pb, False, steps=1)
+    _, pri = _run(pb, True, steps=1)
+    old = os.environ.get('CMPC_QP_SPLIT_FRESH')
+    os.environ['CMPC_QP_SPLIT_FRESH'] = '0'
+    try:
+        _, off = _run(pb, True, steps=1)
+    finally:
+        if old is None:
+            os.environ.pop('CMPC_QP_SPLIT_FRESH', None)
+        else:
+            os.environ['CMPC_QP_SPLIT_FRESH'] = old
+    (z1, s1, i1, _, _), (z2, s2, i2, _, t2), (z3, s3, i3, _, t3) = one[0], pri[0], off[0]
+    assert np.all(t3 == 0)
+    np.testing.assert_array_equal(z1, z3)
+    assert np.all(s2 == 1) and np.abs(i1 - i2).max() <= 1
+    np.testing.assert_array_equal(t2 > 0, i2 > 6)
+    assert (t2 > 0).sum() > 0
+    err = np.abs(z1 - z2).max(axis=1) / np.abs(z1).max(axis=1)
+    assert err.max() <= 1e-7, err.max()
