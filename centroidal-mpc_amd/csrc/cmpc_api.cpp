@@ -202,11 +202,10 @@ double qp_step_fraction(cmpc_handle h) {
     return h->robot == 1 ? 0.995 : 0.999;
 }
 
-// Stopping tolerances: the settings, or (0) the robot's.  fp64: Solo12 1e-9 with complementarity
-// against the primal scale, TALOS 1e-10 (qp_ipm.hip COMP_PRIMAL_SCALE); fp32 1e-6.
+// Stopping tolerances: the settings, or (0) the default: fp64 1e-10, fp32 1e-6 (qp_ipm.hip
+// COMP_PRIMAL_SCALE for Solo12's complementarity after a rejected polish).
 double qp_eps_default(cmpc_handle h) {
-    if (h->prec != CMPC_PREC_F64) return 1e-6;
-    return h->robot == 1 ? 1e-10 : 1e-9;
+    return h->prec != CMPC_PREC_F64 ? 1e-6 : 1e-10;
 }
 double qp_eps_env() {   // CMPC_QP_EPS: diagnostic override of both tolerances (A/B runs)
     const char *e = std::getenv("CMPC_QP_EPS");

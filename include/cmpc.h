@@ -106,8 +106,8 @@ typedef struct {
 /* QP solver settings (defaults by cmpc_default_qp_settings) */
 typedef struct {
     int32_t max_iter;       /* interior-point iterations (default 60) */
-    double eps_abs;         /* absolute tolerance; 0 (default): the robot's -- fp64 Solo12 1e-9 (its
-                             * complementarity measured against the primal scale), TALOS 1e-10; fp32 1e-6 */
+    double eps_abs;         /* absolute tolerance; 0 (default): fp64 1e-10, fp32 1e-6 (Solo12 fp64: after a
+                             * rejected polish, complementarity against 10x the primal tolerance) */
     double eps_rel;         /* relative tolerance; 0 (default): as eps_abs */
     double step_fraction;   /* fraction-to-boundary in (0, 1); 0 (default) picks the robot's:
                              * Solo12 0.999, TALOS 0.995 (same-box measured) */

@@ -93,9 +93,9 @@ INIT_FLOOR_L = 0.1        # lambda floor
 
 def robot_defaults(qp):
     """The kernel's default fp64 stopping and polishing tolerances for the QP's robot (cmpc_api.cpp
-    qp_eps_default / qp_polish_eps): Solo12 eps 1e-9, polish 1e-7; TALOS 1e-10, no polishing (0; the
-    mirror's tests of TALOS polishing pass their own tolerance)."""
-    return (1e-9, 1e-7) if qp.robot == 'solo12' else (1e-10, 0.0)
+    qp_eps_default / qp_polish_eps): eps 1e-10; Solo12 polishes at 1e-7, TALOS not (0; the mirror's
+    tests of TALOS polishing pass their own tolerance)."""
+    return (1e-10, 1e-7) if qp.robot == 'solo12' else (1e-10, 0.0)
 
 
 def solve(qp, eps=1e-11, max_iter=60, eta=0.999, verbose=False, reg=0.0, piv_floor=1e-13, dcap_rel=1e12,
@@ -213,7 +213,10 @@ def solve(qp, eps=1e-11, max_iter=60, eta=0.999, verbose=False, reg=0.0, piv_flo
                       np.abs(qp.Wu * u).max(), np.abs(eu).max(), np.abs(gu).max(), 1.0)
         # complementarity against the primal scale on Solo12, the dual scale on TALOS (qp_ipm.hip
         # COMP_PRIMAL_SCALE)
-        scale_c = scale_p if (comp_primal if comp_primal is not None else not talos) else scale_d
+        # (Solo12: 10x the primal tolerance once a polish was rejected, or with polishing off)
+        strict = (comp_primal if comp_primal is not None else
+                  (not talos and (not polish or any(pl['status'] < 0 for pl in polish_log))))
+        scale_c = 10.0 * scale_p if strict else scale_d
         hist.append((it, prim, dual, comp, mu_))
         if verbose:
             print('it %2d prim %.2e dual %.2e comp %.2e mu %.2e' % (it, prim, dual, comp, mu_))
