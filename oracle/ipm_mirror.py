@@ -227,6 +227,16 @@ def solve(qp, eps=1e-11, max_iter=60, eta=0.999, verbose=False, reg=0.0, piv_flo
         if not init and merit <= 1.0:
             status = 1
             break
+        # (the kernel's second attempt after a rejected guess, once the dual-scale test at eps holds)
+        if strict and polish and len(polish_log) == 1 and not init and \
+                max(prim / (eps * scale_p), dual / (eps * scale_d), comp / (eps * scale_d)) <= 1.0:
+            pol = _polish(qp, masks, x, u, t, nu_, s, lam, last, system_at, GT, ET, Ez, ineq_val, e_rhs,
+                          polish_eps, talos, polish_rel)
+            polish_log.append(pol)
+            if pol['status'] == 1:
+                x, u, t, nu_, lam, s = pol['x'], pol['u'], pol['t'], pol['nu'], pol['lam'], pol['s']
+                status = 1
+                break
         # solution polishing once the iterate meets eps_polish (looser than eps): accepted -> done;
         # rejected -> the interior-point iterations go on to eps
         if polish and not polished_try and not init and it > 1 and merit * eps / polish_eps <= 1.0:
