@@ -225,13 +225,17 @@ double qp_eps_rel(cmpc_handle h) {
 // steps against 5.48 without, 281.8k SCP it/s against 276.8k (1e-8: 273.0k).  TALOS (BASELINE C4
 // from its fourth SCP iteration) guesses wrong on 384 of 512 at 1e-7 and 99-166 at 1e-8 / 1e-9, where
 // every rejected polish costs a factorization: 51.7k against 54.3k without, so TALOS does not polish.
-// fp32 (C3) is not polished.
+// fp32 (C3) is not polished.  Round-4 sweep with the final stopping rule (profiles/r04d_polish_sweep2.log):
+// split launches (the metric config) 1e-7 324k, 3e-8 312k, 1e-8 300k; four waves per problem without a
+// split (C2, the 4- and 8-GPU shards), where the launch lasts as long as its slowest problem and a
+// rejected first guess lands on it, 1e-7 166k (3 rejected), 3e-8 262k (none), 1e-8 229k.
 double qp_polish_eps(cmpc_handle h) {
     if (h->prec != CMPC_PREC_F64) return 0.0;
     if (const char *e = std::getenv("CMPC_QP_POLISH_EPS"))   // diagnostic override (A/B runs)
         return std::atof(e);
     if (h->qs.polish_eps >= 0) return h->qs.polish_eps;
-    return h->robot == 1 ? 0.0 : 1e-7;
+    if (h->robot == 1) return 0.0;
+    return qp_split(h) ? 1e-7 : 3e-8;
 }
 
 // Covariance scan placement.  Sigma feeds only the chance-constraint back-off of stochastic

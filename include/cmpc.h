@@ -123,7 +123,7 @@ typedef struct {
      * the iterate meets this tolerance (relative and absolute, like eps), the equality-constrained
      * QP on the guessed active set is solved with one more factorization; accepted when the
      * polished point meets eps with s, lambda >= 0 (then it is the exact minimizer), else the
-     * interior-point iterations go on.  < 0 (default): the robot's (fp64 Solo12 1e-7, TALOS off;
+     * interior-point iterations go on.  < 0 (default): the robot's (fp64 Solo12 1e-7 with split launches, 3e-8 without; TALOS off;
      * fp32 off); 0: off */
     double polish_eps;
 } cmpc_qp_settings;

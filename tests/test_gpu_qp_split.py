@@ -41,7 +41,8 @@ class _split:
 def _run(pb, on, steps=3, waves=1):
     with _split(on):
         s = Solver(pb.robot, pb.N, pb.B, 'fp64')
-        s.set_qp_settings(waves_per_problem=waves)
+        # (the same polishing tolerance either way: its default depends on whether the launch splits)
+        s.set_qp_settings(waves_per_problem=waves, polish_eps=0.0 if str(pb.robot).lower() == 'talos' else 1e-7)
         s.upload(pb)
         kernel = s.qp_kernel()
         out = []
@@ -97,7 +98,7 @@ def test_split_early_exit_path(cfg, N, B):
     for on in (False, True):
         with _split(on):
             s = Solver(pb.robot, N, B, 'fp64')
-            s.set_qp_settings(waves_per_problem=1)
+            s.set_qp_settings(waves_per_problem=1, polish_eps=0.0 if str(pb.robot).lower() == 'talos' else 1e-7)
             s.upload(pb)
             s.solve_scp(fixed_iters=False)
             res[on] = (s.solution(with_ks=False), s.iteration_history())
