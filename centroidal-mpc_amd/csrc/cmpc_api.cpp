@@ -179,7 +179,19 @@ int qp_split(cmpc_handle h) {
     if (const char *e = std::getenv("CMPC_QP_SPLIT"))
         if (e[0] == '0') return 0;
     if (w == 2 && h->N < 40) return 0;   // (a two-wave head needs the four-wave tail)
+    if (const char *e = std::getenv("CMPC_QP_TAIL_WAVES"))   // diagnostic override (A/B runs)
+        if (e[0] == '2' && w == 1) return 2;
     return h->N >= 40 ? 4 : 2;
+}
+
+// Tail capacity of a split launch: the problems one round of the tail holds, a SIMD per wave
+// (n_cu problems on four waves, 2 n_cu on two).  CMPC_QP_SPLIT_CAP overrides (A/B runs).
+int qp_split_cap(cmpc_handle h, int tw) {
+    if (const char *e = std::getenv("CMPC_QP_SPLIT_CAP")) {
+        const int c = std::atoi(e);
+        if (c > 0) return c;
+    }
+    return h->n_cu * 4 / tw;
 }
 
 // Yield iteration of a split launch on a never-solved batch (the reference's use: every solve_scp
@@ -375,8 +387,8 @@ template <typename T, int R> void launch_phase(cmpc_handle h, int phase, int onl
         if constexpr (sizeof(T) == 8) {
             if (tw) {   // split launches: head (one wave per problem, the slowest leave), tail
                 int *sp = (int *)h->qp_split;
-                hipLaunchKernelGGL((k_qp_split<T>), dim3(1), dim3(1024), 0, h->stream, d, only_active, h->n_cu,
-                                   qp_split_prior(h), sp);
+                hipLaunchKernelGGL((k_qp_split<T>), dim3(1), dim3(1024), 0, h->stream, d, only_active,
+                                   qp_split_cap(h, tw), qp_split_prior(h), sp);
                 if (nt == 128) {   // two-wave head (BASELINE C4: TALOS N=200 x 512)
                     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_qp_ipm<T, R, 128, 1>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
