@@ -184,14 +184,15 @@ int qp_split(cmpc_handle h) {
     return h->N >= 40 ? 4 : 2;
 }
 
-// Tail capacity of a split launch: the problems one round of the tail holds, a SIMD per wave
-// (n_cu problems on four waves, 2 n_cu on two).  CMPC_QP_SPLIT_CAP overrides (A/B runs).
+// Tail capacity of a split launch: at most one problem per CU in the tail (k_qp_split).
+// CMPC_QP_SPLIT_CAP overrides (A/B runs: profiles/r04e_tail_shape_ab.log).
 int qp_split_cap(cmpc_handle h, int tw) {
+    (void)tw;
     if (const char *e = std::getenv("CMPC_QP_SPLIT_CAP")) {
         const int c = std::atoi(e);
         if (c > 0) return c;
     }
-    return h->n_cu * 4 / tw;
+    return h->n_cu;
 }
 
 // Yield iteration of a split launch on a never-solved batch (the reference's use: every solve_scp
