@@ -115,9 +115,11 @@ typedef struct {
      * floored row by row at these values (default 0.1, 0.1); 0 selects CVXOPT's shift of every
      * row by 1 + the largest violation, which TALOS handles always use */
     double init_floor_s, init_floor_l;
-    /* waves per problem of the QP workgroup: 1 (knots k, k + 64, ... on one wave) or 2 (the
-     * per-knot phases on two waves, the Schur recurrence on the first); 0 (default) picks 2 when
-     * two waves per problem still fit the device in one round (2 B <= 4 x CUs) and N + 1 > 64 */
+    /* waves per problem of the QP workgroup: 1 (knots k, k + 64, ... on one wave), 2 (the
+     * per-knot phases on two waves, one end of the Schur recurrence on each) or 4 (four chains of
+     * the recurrence, N >= 16; shorter horizons get 2); 0 (default) picks 4 when every problem
+     * gets a CU of its own and N >= 40, else 2 when two waves per problem still fit the device in
+     * one round (2 B <= 4 x CUs) and N + 1 > 64, else 1 */
     int32_t waves_per_problem;
     /* solution polishing, as the reference's OSQP setup (polish=True, src/scp_solver.py:62): once
      * the iterate meets this tolerance (relative and absolute, like eps), the equality-constrained
